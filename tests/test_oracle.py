@@ -1,0 +1,56 @@
+"""Pin the CPU oracle against the reference's own outputs (golden fixtures)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import FIXTURES, load_fixture, oracle_cfg
+from oracle import berson_oracle as O
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_pairs_match_reference(name):
+    meta, d, _ = load_fixture(name)
+    pair = O.prepare_berson_inputs(d["input_ids"], d["labels"], meta["config"]["N"])
+    for k, v in pair.items():
+        np.testing.assert_array_equal(v, d["pair::" + k], err_msg=k)
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_loss_and_grads_match_reference(name):
+    meta, d, params = load_fixture(name)
+    cfg = oracle_cfg(meta)
+    p = {k: v.clone().requires_grad_(v.dtype.is_floating_point) for k, v in params.items()}
+    images = torch.from_numpy(d["images"])
+    loss, pair, enc = O.forward_loss(p, d["input_ids"], d["labels"], images, cfg)
+    assert abs(loss.item() - float(d["loss"])) < 1e-5, (loss.item(), float(d["loss"]))
+    loss.backward()
+    gsq = 0.0
+    for k, v in p.items():
+        if v.grad is not None:
+            gsq += float((v.grad.double() ** 2).sum())
+    assert abs(gsq ** 0.5 - float(d["grad_norm"])) < 1e-4 * float(d["grad_norm"])
+    n = 0
+    for k in d:
+        if k.startswith("g::"):
+            g = p[k[3:]].grad
+            ref = d[k]
+            if g is None:
+                assert np.abs(ref).max() == 0, k
+                continue
+            np.testing.assert_allclose(g.numpy(), ref, rtol=2e-3, atol=2e-6, err_msg=k)
+            n += 1
+    assert n > 10
+    np.testing.assert_allclose(enc["lang"].detach().numpy(), d["i::lang_feats"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(enc["okey"].detach().numpy(), d["i::original_key"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_beam_order_matches_reference(name):
+    meta, d, params = load_fixture(name)
+    cfg = oracle_cfg(meta)
+    images = torch.from_numpy(d["images"])
+    with torch.no_grad():
+        for b in range(d["input_ids"].shape[0]):
+            pair = O.prepare_berson_inputs(d["input_ids"][b:b + 1], d["labels"][b:b + 1], cfg["N"])
+            enc = O.encode(params, pair, images[b:b + 1], cfg)
+            assert O.beam_order(params, enc) == list(d["order"][b])
