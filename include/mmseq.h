@@ -1,0 +1,242 @@
+/*
+ * mmseq — MI355X-native (gfx950 / CDNA4) kernels for the multimodal sequence-ordering hot path
+ * of telin0411/multimodal_sequencing (CLIP-ViT -> VisualBERT-style LXRT encoder -> BERSON).
+ *
+ * C ABI: plain pointers and sizes, no torch types. Every entry point is stream-ordered on the
+ * caller's hipStream_t, performs no host synchronisation and no allocation: the caller owns all
+ * input, output and workspace buffers. Functions are stateless and reentrant. On failure they
+ * return a negative mmseq_status and mmseq_last_error() describes it (thread-local).
+ *
+ * The reference has NO native layer: it is 100 % PyTorch, so each entry point
+ * below replaces a group of PyTorch ops at the reference site cited next to it. The Python
+ * binding that a maintainer adds on the reference side is shown in INTEGRATION.md.
+ *
+ * Dtypes: MMSEQ_F32 (exact fp32 "parity mode": fp32 MFMA v_mfma_f32_16x16x4_f32) and
+ * MMSEQ_BF16 (perf mode: bf16 operands, fp32 accumulate, v_mfma_f32_16x16x32_bf16).
+ */
+#ifndef MMSEQ_H
+#define MMSEQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mmseq_stream;  /* == hipStream_t; NULL = default stream */
+typedef int mmseq_status;
+enum { MMSEQ_OK = 0, MMSEQ_EINVAL = -1, MMSEQ_EUNSUPPORTED = -2, MMSEQ_EHIP = -3 };
+typedef enum { MMSEQ_F32 = 0, MMSEQ_BF16 = 1 } mmseq_dtype;
+
+/* Activations fused into GEMM epilogues / elementwise kernels:
+ *   GELU_ERF   lxrt/modeling.py:116-122 (BertIntermediate)
+ *   QUICKGELU  clip/model.py:199-201     (ViT MLP)
+ *   TANH       berson/modeling_bert.py:699 (HierarchicalAttention.sentence_tran)
+ *   GELU_TANH  berson/neural.py:7-8      (PositionwiseFeedForward) */
+typedef enum {
+  MMSEQ_ACT_NONE = 0, MMSEQ_ACT_GELU_ERF = 1, MMSEQ_ACT_QUICKGELU = 2, MMSEQ_ACT_TANH = 3,
+  MMSEQ_ACT_GELU_TANH = 4
+} mmseq_act;
+
+const char* mmseq_last_error(void);
+const char* mmseq_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * GEMM (replaces every nn.Linear / matmul on the path: lxrt/modeling.py:385-395,437,473,491,
+ * 576; clip/model.py:208-214,263,304; berson/modeling_bert.py:697-701,745,882-902; neural.py).
+ *
+ *   C[b][m][n] = epilogue( alpha * sum_k A(m,k) * B(k,n) )        b < batch
+ *   layout "NT" (trans=0): A(m,k) = A[m*lda + k],  B(k,n) = B[n*ldb + k]   (both K-contiguous)
+ *   layout "TN" (trans=1): A(m,k) = A[k*lda + m],  B(k,n) = B[k*ldb + n]   (both M/N-contiguous)
+ *   epilogue, in order:  v += bias[n] (f32, optional)
+ *                        if dact_aux: v *= act'(dact_aux[m][n])          (backward through act)
+ *                        else if act: aux_out[m][n] = v (optional); v = act(v)
+ *                        v += resid[m][n] (optional)   ;   if accumulate: v += C[m][n]
+ *   A, B share in_dtype; C, resid, aux_out, dact_aux share out_dtype (aux ld = ldc).
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch,
+                        const void* A, int64_t lda, int64_t strideA,
+                        const void* B, int64_t ldb, int64_t strideB,
+                        void* C, int64_t ldc, int64_t strideC,
+                        const float* bias, int act, void* aux_out, const void* dact_aux,
+                        const void* resid, int64_t ldr, int64_t strideR,
+                        float alpha, int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
+                        mmseq_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused multi-head attention over a packed QKV activation (lxrt/modeling.py:398-425 with the
+ * additive key mask of :1537-1545 / :1071-1094; clip/model.py:219-221 nn.MultiheadAttention).
+ *   token t of sequence p has row  qkv + (p*T + t)*ld_qkv ; head h of Q at +q_off + h*64,
+ *   K at +k_off + h*64, V at +v_off + h*64. head_dim is 64.
+ *   key_bias: [P][T] f32 additive (0 or -10000), or NULL.  out row: out + (p*T+t)*ld_out + h*64.
+ *   lse: [P][heads][T] f32 (log-sum-exp of the scaled, biased scores), written by fwd.
+ * bwd: delta workspace [P][heads][T] f32; dqkv has the same packed layout as qkv (ld_dqkv).
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                            int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
+                            float scale, void* out, int64_t ld_out, float* lse,
+                            mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                            int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
+                            float scale, const void* out, int64_t ld_out, const void* dout,
+                            int64_t ld_dout, const float* lse, float* delta, void* dqkv,
+                            int64_t ld_dqkv, mmseq_dtype dtype, mmseq_stream stream);
+
+/* Small multi-head attention for the BERSON inter-sentence encoder (neural.py:98-235):
+ * [B][T][heads*d] separate q/k/v tensors, T <= 64, d <= 128, fp32, key_bias [B][T] or NULL.
+ * probs [B][heads][T][T] are saved by fwd for bwd. */
+mmseq_status mmseq_small_attn_fwd(int B, int T, int heads, int d, const float* q, const float* k,
+                                  const float* v, const float* key_bias, float scale, float* out,
+                                  float* probs, mmseq_stream stream);
+mmseq_status mmseq_small_attn_bwd(int B, int T, int heads, int d, const float* q, const float* k,
+                                  const float* v, const float* probs, const float* dout,
+                                  float scale, float* dq, float* dk, float* dv,
+                                  mmseq_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * LayerNorm over the last dim (cols), fp32 statistics (lxrt BertLayerNorm eps 1e-12:
+ * :353,432,486,577; CLIP fp32 LayerNorm eps 1e-5: clip/model.py:190-196; BERSON eps 1e-6).
+ * Row r lives at base + (r / rpb)*bstride + (r % rpb)*ld  (two-level strides let the kernels
+ * read/write the text or visual half of the joint [P][T][H] buffer in place; rpb = rows
+ * per batch).  bwd: dx = LN'(dy) (+ dres if non-NULL); dgamma/dbeta ACCUMULATE (+=) and need a
+ * workspace of mmseq_layernorm_bwd_workspace(rows, cols) floats.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int64_t ld;       /* row stride (elements) inside a batch */
+  int64_t bstride;  /* batch stride (elements) */
+  int64_t rpb;      /* rows per batch */
+} mmseq_rows;
+
+mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, mmseq_rows xl,
+                                 const float* gamma, const float* beta, float eps, void* y,
+                                 mmseq_rows yl, float* mean, float* rstd, mmseq_dtype x_dtype,
+                                 mmseq_dtype y_dtype, mmseq_stream stream);
+int64_t mmseq_layernorm_bwd_workspace(int rows, int cols);
+mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                 const void* x, mmseq_rows xl, const float* mean,
+                                 const float* rstd, const float* gamma, void* dx, mmseq_rows dxl,
+                                 const void* dres, mmseq_rows dresl, float* dgamma, float* dbeta,
+                                 float* workspace, mmseq_dtype dtype, mmseq_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused text embedding + LayerNorm written straight into the joint buffer (BertEmbeddings,
+ * lxrt/modeling.py:356-370; joint concat :1093): for pair p, token t < Lt:
+ *   e = word[ids] + pos[t] + type[tt];  joint row (p*ld_pair + t) = LN(e)   (eps as given)
+ * bwd recomputes e, applies LN backward and scatters into dword/dpos/dtype (+=), skipping
+ * row 0 of every table (padding_idx = 0 on all three, :347-349). dgamma/dbeta accumulate.
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* ids, const int64_t* tt,
+                                const float* word, const float* pos, const float* type,
+                                const float* gamma, const float* beta, float eps, void* joint,
+                                int64_t ld_pair, float* mean, float* rstd, mmseq_dtype dtype,
+                                mmseq_stream stream);
+mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* ids, const int64_t* tt,
+                                const float* word, const float* pos, const float* type,
+                                const float* gamma, const float* mean, const float* rstd,
+                                const void* djoint, int64_t ld_pair, float* dword, float* dpos,
+                                float* dtype_tab, float* dgamma, float* dbeta, float* workspace,
+                                mmseq_dtype dtype, mmseq_stream stream);
+int64_t mmseq_embed_ln_bwd_workspace(int P, int Lt, int H);
+
+/* ------------------------------------------------------------------------------------------
+ * ViT patch path (clip/model.py:262-278 with the img_len=2 quirk).
+ *  im2col: images [B][N][3][R][R] f32 + pairs [B][npair][2] -> patches [B*npair][2*g*g][3*ps*ps]
+ *          (pair images gathered on device: no 8x duplicated H2D copy, process_images :82-97)
+ *  embed_fwd: x[p][0] = cls + pos[0]; x[p][1+j] = patch_out[p][j] + pos[j < g*g ? 1+j : j-g*g]
+ *             y = LN(x) (ln_pre, eps)   (x saved for bwd as dtype)
+ *  embed_bwd: dx = LN'(dy); dcls += sum_p dx[p][0]; dpos[r] += sum of its tokens;
+ *             dpatch_out[p][j] = dx[p][1+j]
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_vit_im2col(int B, int N, int npair, int R, int ps, const float* images,
+                              const int64_t* pairs, void* patches, mmseq_dtype dtype,
+                              mmseq_stream stream);
+mmseq_status mmseq_vit_embed_fwd(int P, int ntok, int W, int npatch_img, const void* patch_out,
+                                 const float* cls, const float* pos, const float* gamma,
+                                 const float* beta, float eps, void* x, void* y, float* mean,
+                                 float* rstd, mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_vit_embed_bwd(int P, int ntok, int W, int npatch_img, const void* dy,
+                                 const void* x, const float* mean, const float* rstd,
+                                 const float* gamma, void* dpatch_out, float* dcls, float* dpos,
+                                 float* dgamma, float* dbeta, float* workspace, mmseq_dtype dtype,
+                                 mmseq_stream stream);
+int64_t mmseq_vit_embed_bwd_workspace(int P, int ntok, int W);
+
+/* ------------------------------------------------------------------------------------------
+ * Elementwise / reduction utilities.
+ * ------------------------------------------------------------------------------------------ */
+/* dst[i] = (dst_dtype) src[i] (f32 <-> bf16, or copy), n elements */
+mmseq_status mmseq_cast(int64_t n, const void* src, mmseq_dtype src_dtype, void* dst,
+                        mmseq_dtype dst_dtype, mmseq_stream stream);
+/* dst[c][r] = src[r][c] for an f32 [rows][cols] matrix, written as dst_dtype */
+mmseq_status mmseq_transpose_cast(int rows, int cols, const float* src, void* dst,
+                                  mmseq_dtype dst_dtype, mmseq_stream stream);
+/* out[c] (+)= sum_r x[r][c] in f32 (bias gradients); rows at x + r*ldx. */
+mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t ldx, float* out,
+                          int accumulate, float* workspace, mmseq_dtype dtype,
+                          mmseq_stream stream);
+int64_t mmseq_colsum_workspace(int rows, int cols);
+/* y = act(x) and dx = dy * act'(x), n elements, same dtype */
+mmseq_status mmseq_act_fwd(int64_t n, int act, const void* x, void* y, mmseq_dtype dtype,
+                           mmseq_stream stream);
+mmseq_status mmseq_act_bwd(int64_t n, int act, const void* z, const void* dy, void* dz,
+                           mmseq_dtype dtype, mmseq_stream stream);
+/* sum of squares of n f32 values into out[0] (overwrite), two-pass deterministic */
+mmseq_status mmseq_sumsq(int64_t n, const float* x, float* out, float* workspace,
+                         mmseq_stream stream);
+int64_t mmseq_sumsq_workspace(int64_t n);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused AdamW over the flat fp32 parameter buffer (transformers 3.4 AdamW as used at
+ * trainers/train.py:172-190,353-363: correct_bias=True, decoupled weight decay applied after
+ * the Adam update, grads pre-scaled by clip_grad_norm_(max_norm) computed from sumsq).
+ *   clip = min(1, max_norm / (sqrt(*sumsq) + 1e-6)) if max_norm > 0 else 1
+ *   m = b1*m + (1-b1)*g*clip ; v = b2*v + (1-b2)*(g*clip)^2
+ *   p -= lr * (m/(1-b1^t)) / (sqrt(v/(1-b2^t)) + eps) ... (HF form: step = lr*sqrt(1-b2^t)/(1-b1^t))
+ *   p -= lr * wd * p   (for elements with decay_mask != 0; decay_mask may be NULL = all decay)
+ * Optionally writes the bf16 shadow copy of the updated parameters (shadow may be NULL).
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_adamw(int64_t n, float* p, const float* g, float* m, float* v,
+                         const uint8_t* decay_mask, float lr, float beta1, float beta2, float eps,
+                         float weight_decay, int step, float max_norm, const float* sumsq,
+                         void* shadow_bf16, mmseq_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * BERSON pointer scoring (modeling_bert.py:1083-1142, the "pointer-score GEMM" epilogue):
+ *   e[b][t][j] = sum_h w[h] * tanh(q[b][t][h] + key[b][t][j][h] + okey[b][j][h]) + w_bias[0]
+ *   (w_bias is a device pointer, may be NULL)
+ *   e = -1e9 where pointed[b][t][j] != 0 or j >= tgt_len[b];  logp = log_softmax_j(e)
+ *   nll[b][t] = -logp[b][t][target[b][t]] if t < tgt_len[b] else 0
+ * bwd: given dnll[b][t] (upstream grad of each nll) WRITE dq, dkey and ACCUMULATE (+=, float
+ * atomics) dokey, dw, dw_bias. Shapes: q [B][N][H], key [B][N][N][H], okey [B][N][H] (f32).
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_pointer_fwd(int B, int N, int H, const float* q, const float* key,
+                               const float* okey, const float* w, const float* w_bias,
+                               const uint8_t* pointed, const int64_t* tgt_len,
+                               const int64_t* target, float* logp, float* nll,
+                               mmseq_stream stream);
+mmseq_status mmseq_pointer_bwd(int B, int N, int H, const float* q, const float* key,
+                               const float* okey, const float* w, const float* logp,
+                               const uint8_t* pointed, const int64_t* tgt_len, const int64_t* target, const float* dnll,
+                               float* dq, float* dkey, float* dokey, float* dw, float* dw_bias,
+                               mmseq_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * HierarchicalAttention span pooling (modeling_bert.py:703-741) without host loops:
+ *   for pair p, span s in {0,1}: mask_s(t) = 1 for t in [1, sep0] (s=0) / [sep0+1, sep1] (s=1)
+ *   a[p][s][t] = mask ? score[p][t] : -10000 ; probs = softmax_t(a); mix[p][s] = probs @ top[p]
+ *   top rows: top + p*ld_pair + t*H. probs saved [P][2][Lt] f32 for bwd.
+ * bwd: dscore[p][t] = sum_s mask*probs*(dmix.top - sum_t' probs*dmix.top) (written);
+ *      dtop[p][t] += probs^T dmix (accumulated in place)
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_span_pool_fwd(int P, int Lt, int H, const void* top, int64_t ld_pair,
+                                 const float* score, const int64_t* sep, float* probs,
+                                 float* mix, mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_span_pool_bwd(int P, int Lt, int H, const void* top, int64_t ld_pair,
+                                 const float* probs, const int64_t* sep, const float* dmix,
+                                 float* dscore, void* dtop, mmseq_dtype dtype,
+                                 mmseq_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMSEQ_H */

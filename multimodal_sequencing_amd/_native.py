@@ -1,0 +1,295 @@
+"""ctypes binding of the mmseq C ABI (include/mmseq.h) — the only path to the HIP kernels.
+
+There is deliberately no fallback: if `_lib/libmmseq.so` is missing or a kernel returns an
+error, the call raises. Every wrapper takes torch tensors that already live on the current HIP
+device and launches on torch's current stream.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libmmseq.so")
+
+F32, BF16 = 0, 1
+ACT = {"none": 0, "gelu": 1, "quickgelu": 2, "tanh": 3, "gelu_tanh": 4}
+
+_c_i64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+
+
+class Rows(ctypes.Structure):
+    """mmseq_rows: row r at base + (r // rpb) * bstride + (r % rpb) * ld (elements)."""
+    _fields_ = [("ld", ctypes.c_int64), ("bstride", ctypes.c_int64), ("rpb", ctypes.c_int64)]
+
+
+def rows(ld, bstride=0, rpb=1 << 62):
+    return Rows(ld, bstride, rpb)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "mmseq_last_error": (ctypes.c_char_p, []),
+    "mmseq_version": (ctypes.c_char_p, []),
+    "mmseq_gemm": (ctypes.c_int, [ctypes.c_int] * 5 + [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
+                                                       _vp, _c_i64, _c_i64, _vp, ctypes.c_int, _vp,
+                                                       _vp, _vp, _c_i64, _c_i64, ctypes.c_float,
+                                                       ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                       _vp]),
+    "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
+                                                           _vp, ctypes.c_float, _vp, _c_i64, _vp,
+                                                           ctypes.c_int, _vp]),
+    "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
+                                                           _vp, ctypes.c_float, _vp, _c_i64, _vp,
+                                                           _c_i64, _vp, _vp, _vp, _c_i64,
+                                                           ctypes.c_int, _vp]),
+    "mmseq_small_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 4 + [ctypes.c_float, _vp,
+                                                                             _vp, _vp]),
+    "mmseq_small_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float, _vp,
+                                                                             _vp, _vp, _vp]),
+    "mmseq_layernorm_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, _vp,
+                                           ctypes.c_float, _vp, Rows, _vp, _vp, ctypes.c_int,
+                                           ctypes.c_int, _vp]),
+    "mmseq_layernorm_bwd_workspace": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
+    "mmseq_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
+                                           _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
+                                           ctypes.c_int, _vp]),
+    "mmseq_embed_ln_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 7 + [ctypes.c_float, _vp,
+                                                                           _c_i64, _vp, _vp,
+                                                                           ctypes.c_int, _vp]),
+    "mmseq_embed_ln_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 9 + [_c_i64] + [_vp] * 6 +
+                           [ctypes.c_int, _vp]),
+    "mmseq_embed_ln_bwd_workspace": (ctypes.c_int64, [ctypes.c_int] * 3),
+    "mmseq_vit_im2col": (ctypes.c_int, [ctypes.c_int] * 5 + [_vp, _vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_vit_embed_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float] +
+                            [_vp] * 4 + [ctypes.c_int, _vp]),
+    "mmseq_vit_embed_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 11 + [ctypes.c_int, _vp]),
+    "mmseq_vit_embed_bwd_workspace": (ctypes.c_int64, [ctypes.c_int] * 3),
+    "mmseq_cast": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp]),
+    "mmseq_transpose_cast": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, ctypes.c_int,
+                                            _vp]),
+    "mmseq_colsum": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _c_i64, _vp, ctypes.c_int,
+                                    _vp, ctypes.c_int, _vp]),
+    "mmseq_colsum_workspace": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
+    "mmseq_act_fwd": (ctypes.c_int, [_c_i64, ctypes.c_int, _vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_act_bwd": (ctypes.c_int, [_c_i64, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_sumsq": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp]),
+    "mmseq_sumsq_workspace": (ctypes.c_int64, [_c_i64]),
+    "mmseq_adamw": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp] + [ctypes.c_float] * 5 +
+                    [ctypes.c_int, ctypes.c_float, _vp, _vp, _vp]),
+    "mmseq_pointer_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 5 + [_vp] * 5 + [_vp]),
+    "mmseq_pointer_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 14 + [_vp]),
+    "mmseq_span_pool_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
+                                                                ctypes.c_int, _vp]),
+    "mmseq_span_pool_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
+                                                                _vp, ctypes.c_int, _vp]),
+}
+
+EXPORTS = sorted(k for k in _SIGS)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"mmseq HIP library not found at {LIB_PATH}; run __graft_entry__.build() "
+                "(make -C multimodal_sequencing_amd/csrc). There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(st, what):
+    if st != 0:
+        raise NativeError(f"{what} failed ({st}): {lib().mmseq_last_error().decode()}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dt(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise NativeError(f"unsupported dtype {t.dtype}")
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise NativeError("mmseq kernels need device tensors (no CPU fallback)")
+
+
+# ------------------------------------------------------------------------------------------------
+def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA=0, sB=0, sC=0,
+         bias=None, act=0, aux=None, dact=None, resid=None, ldr=None, sR=0, alpha=1.0,
+         accumulate=False):
+    _dev(A, B, C)
+    if lda is None:
+        lda = M if trans else K
+    if ldb is None:
+        ldb = N if trans else K
+    if ldc is None:
+        ldc = N
+    if ldr is None:
+        ldr = ldc
+    _check(lib().mmseq_gemm(trans, M, N, K, batch, _p(A), lda, sA, _p(B), ldb, sB, _p(C), ldc, sC,
+                            _p(bias), act, _p(aux), _p(dact), _p(resid), ldr, sR, alpha,
+                            int(accumulate), dt(A), dt(C), _stream()), "mmseq_gemm")
+
+
+def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse):
+    _dev(qkv, out, lse)
+    _check(lib().mmseq_attn_fwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
+                                scale, _p(out), ld_out, _p(lse), dt(qkv), _stream()),
+           "mmseq_attn_fwd")
+
+
+def attn_bwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, dout,
+             ld_dout, lse, delta, dqkv, ld_dqkv):
+    _check(lib().mmseq_attn_bwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
+                                scale, _p(out), ld_out, _p(dout), ld_dout, _p(lse), _p(delta),
+                                _p(dqkv), ld_dqkv, dt(qkv), _stream()), "mmseq_attn_bwd")
+
+
+def small_attn_fwd(B, T, heads, d, q, k, v, key_bias, scale, out, probs):
+    _check(lib().mmseq_small_attn_fwd(B, T, heads, d, _p(q), _p(k), _p(v), _p(key_bias), scale,
+                                      _p(out), _p(probs), _stream()), "mmseq_small_attn_fwd")
+
+
+def small_attn_bwd(B, T, heads, d, q, k, v, probs, dout, scale, dq, dk, dv):
+    _check(lib().mmseq_small_attn_bwd(B, T, heads, d, _p(q), _p(k), _p(v), _p(probs), _p(dout),
+                                      scale, _p(dq), _p(dk), _p(dv), _stream()),
+           "mmseq_small_attn_bwd")
+
+
+def layernorm_fwd(nrows, cols, x, xl, gamma, beta, eps, y, yl, mean, rstd):
+    _dev(x, y, gamma, beta)
+    _check(lib().mmseq_layernorm_fwd(nrows, cols, _p(x), xl, _p(gamma), _p(beta), eps, _p(y), yl,
+                                     _p(mean), _p(rstd), dt(x), dt(y), _stream()),
+           "mmseq_layernorm_fwd")
+
+
+def layernorm_bwd(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl, dgamma,
+                  dbeta):
+    ws = torch.empty(lib().mmseq_layernorm_bwd_workspace(nrows, cols), dtype=torch.float32,
+                     device=x.device)
+    _check(lib().mmseq_layernorm_bwd(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
+                                     _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
+                                     _p(dbeta), _p(ws), dt(x), _stream()), "mmseq_layernorm_bwd")
+
+
+def embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gamma, beta, eps, joint, ld_pair, mean, rstd):
+    _check(lib().mmseq_embed_ln_fwd(P, Lt, H, _p(ids), _p(tt), _p(word), _p(pos), _p(typ),
+                                    _p(gamma), _p(beta), eps, _p(joint), ld_pair, _p(mean),
+                                    _p(rstd), dt(joint), _stream()), "mmseq_embed_ln_fwd")
+
+
+def embed_ln_bwd(P, Lt, H, ids, tt, word, pos, typ, gamma, mean, rstd, djoint, ld_pair, dword,
+                 dpos, dtyp, dgamma, dbeta):
+    ws = torch.empty(lib().mmseq_embed_ln_bwd_workspace(P, Lt, H), dtype=torch.float32,
+                     device=djoint.device)
+    _check(lib().mmseq_embed_ln_bwd(P, Lt, H, _p(ids), _p(tt), _p(word), _p(pos), _p(typ),
+                                    _p(gamma), _p(mean), _p(rstd), _p(djoint), ld_pair, _p(dword),
+                                    _p(dpos), _p(dtyp), _p(dgamma), _p(dbeta), _p(ws),
+                                    dt(djoint), _stream()), "mmseq_embed_ln_bwd")
+
+
+def vit_im2col(B, N, npair, R, ps, images, pairs, patches):
+    _check(lib().mmseq_vit_im2col(B, N, npair, R, ps, _p(images), _p(pairs), _p(patches),
+                                  dt(patches), _stream()), "mmseq_vit_im2col")
+
+
+def vit_embed_fwd(P, ntok, W, npatch, patch_out, cls, pos, gamma, beta, eps, x, y, mean, rstd):
+    _check(lib().mmseq_vit_embed_fwd(P, ntok, W, npatch, _p(patch_out), _p(cls), _p(pos),
+                                     _p(gamma), _p(beta), eps, _p(x), _p(y), _p(mean), _p(rstd),
+                                     dt(x), _stream()), "mmseq_vit_embed_fwd")
+
+
+def vit_embed_bwd(P, ntok, W, npatch, dy, x, mean, rstd, gamma, dpatch, dcls, dpos, dgamma, dbeta):
+    ws = torch.empty(lib().mmseq_vit_embed_bwd_workspace(P, ntok, W), dtype=torch.float32,
+                     device=x.device)
+    _check(lib().mmseq_vit_embed_bwd(P, ntok, W, npatch, _p(dy), _p(x), _p(mean), _p(rstd),
+                                     _p(gamma), _p(dpatch), _p(dcls), _p(dpos), _p(dgamma),
+                                     _p(dbeta), _p(ws), dt(x), _stream()), "mmseq_vit_embed_bwd")
+
+
+def cast(src, dst):
+    assert src.numel() == dst.numel()
+    _check(lib().mmseq_cast(src.numel(), _p(src), dt(src), _p(dst), dt(dst), _stream()),
+           "mmseq_cast")
+
+
+def transpose_cast(src, dst):
+    r, c = src.shape
+    _check(lib().mmseq_transpose_cast(r, c, _p(src), _p(dst), dt(dst), _stream()),
+           "mmseq_transpose_cast")
+
+
+def colsum(x, nrows, cols, ldx, out, accumulate=True):
+    ws = torch.empty(max(1, lib().mmseq_colsum_workspace(nrows, cols)), dtype=torch.float32,
+                     device=x.device)
+    _check(lib().mmseq_colsum(nrows, cols, _p(x), ldx, _p(out), int(accumulate), _p(ws), dt(x),
+                              _stream()), "mmseq_colsum")
+
+
+def act_fwd(x, y, act):
+    _check(lib().mmseq_act_fwd(x.numel(), act, _p(x), _p(y), dt(x), _stream()), "mmseq_act_fwd")
+
+
+def act_bwd(z, dy, dz, act):
+    _check(lib().mmseq_act_bwd(z.numel(), act, _p(z), _p(dy), _p(dz), dt(z), _stream()),
+           "mmseq_act_bwd")
+
+
+def sumsq(x, out):
+    ws = torch.empty(lib().mmseq_sumsq_workspace(x.numel()), dtype=torch.float32, device=x.device)
+    _check(lib().mmseq_sumsq(x.numel(), _p(x), _p(out), _p(ws), _stream()), "mmseq_sumsq")
+
+
+def adamw(p, g, m, v, decay_mask, lr, b1, b2, eps, wd, step, max_norm, sumsq_buf, shadow):
+    _check(lib().mmseq_adamw(p.numel(), _p(p), _p(g), _p(m), _p(v), _p(decay_mask), lr, b1, b2,
+                             eps, wd, step, max_norm, _p(sumsq_buf), _p(shadow), _stream()),
+           "mmseq_adamw")
+
+
+def pointer_fwd(B, N, H, q, key, okey, w, wb, pointed, tgt_len, target, logp, nll):
+    _check(lib().mmseq_pointer_fwd(B, N, H, _p(q), _p(key), _p(okey), _p(w), _p(wb), _p(pointed),
+                                   _p(tgt_len), _p(target), _p(logp), _p(nll), _stream()),
+           "mmseq_pointer_fwd")
+
+
+def pointer_bwd(B, N, H, q, key, okey, w, logp, pointed, tgt_len, target, dnll, dq, dkey, dokey,
+                dw, dwb):
+    _check(lib().mmseq_pointer_bwd(B, N, H, _p(q), _p(key), _p(okey), _p(w), _p(logp),
+                                   _p(pointed), _p(tgt_len), _p(target), _p(dnll), _p(dq), _p(dkey),
+                                   _p(dokey), _p(dw), _p(dwb), _stream()), "mmseq_pointer_bwd")
+
+
+def span_pool_fwd(P, Lt, H, top, ld_pair, score, sep, probs, mix):
+    _check(lib().mmseq_span_pool_fwd(P, Lt, H, _p(top), ld_pair, _p(score), _p(sep), _p(probs),
+                                     _p(mix), dt(top), _stream()), "mmseq_span_pool_fwd")
+
+
+def span_pool_bwd(P, Lt, H, top, ld_pair, probs, sep, dmix, dscore, dtop):
+    _check(lib().mmseq_span_pool_bwd(P, Lt, H, _p(top), ld_pair, _p(probs), _p(sep), _p(dmix),
+                                     _p(dscore), _p(dtop), dt(top), _stream()),
+           "mmseq_span_pool_bwd")

@@ -1,0 +1,553 @@
+// Fused multi-head attention, head_dim 64, flash-style (no T x T materialisation), fwd + bwd.
+// Replaces BertAttention.forward (lxrt/modeling.py:398-425) and nn.MultiheadAttention in the
+// CLIP ViT blocks (clip/model.py:219-221). See include/mmseq.h for the layout contract.
+//
+// Workgroup = 4 waves; each wave owns 16 rows (queries in fwd / dQ, keys in dK/dV); the
+// 64-row tiles of the other operand are staged through LDS ([64][80] bf16: a 160-byte row
+// stride makes both the 16-byte row reads and the ds_read_b64_tr_b16 transposed reads
+// bank-conflict-free). MFMA 16x16x32 bf16 (perf) or 16x16x4 f32 (parity), f32 softmax.
+//
+// fwd  (swapped QK^T, guide §B "Fused attention"): S^T = K Q^T puts the query on the lane and the
+//      keys in registers, so row max / row sum are in-lane plus two xor-shuffles; P^T is then
+//      directly the B operand of O^T = V^T P^T (V^T fragments by transposed reads).
+// bwd  two deterministic kernels (no float atomics):
+//      dkdv: per key tile, sweep the queries: S, dP with the key on the lane; dV^T += dO^T P and
+//            dK^T += Q^T dS take P / dS straight from the accumulators.
+//      dq:   per query tile, sweep the keys with the swapped form; dQ^T += K^T dS^T.
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 64;       // head dim
+constexpr int QT = 64;       // rows per workgroup tile
+constexpr float NEG = -1e30f;
+
+template <typename TI> struct ACfg;
+template <> struct ACfg<unsigned short> { static constexpr int LD = 80, VE = 8; };
+template <> struct ACfg<float> { static constexpr int LD = 68, VE = 4; };
+
+template <typename TI> struct V16;
+template <> struct V16<unsigned short> { typedef u16x8 T; };
+template <> struct V16<float> { typedef f32x4 T; };
+
+struct AttnArgs {
+  int P, T, heads;
+  const void* qkv; int64_t ld_qkv, q_off, k_off, v_off;
+  const float* key_bias; float scale;
+  const void* out; int64_t ld_out;
+  const void* dout; int64_t ld_dout;
+  float* lse; float* delta;
+  void* dqkv; int64_t ld_dqkv;
+  void* o_w;  // fwd output
+};
+
+// Stage rows [r0, r0+64) of one head's 64-wide slice into LDS tile s ([64][LD]); zero-fill >= T.
+template <typename TI>
+__device__ __forceinline__ void stage_tile(TI* s, const TI* base, int64_t ld, int r0, int T,
+                                           int tid) {
+  typedef typename V16<TI>::T V;
+  constexpr int VE = ACfg<TI>::VE, LD = ACfg<TI>::LD;
+  constexpr int CPR = HD / VE;             // chunks per row
+  constexpr int NCH = (QT * CPR) / 256;    // chunks per thread
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int L = c * 256 + tid;
+    int r = L / CPR, cc = L % CPR;
+    V v;
+    if (r0 + r < T) {
+      v = *reinterpret_cast<const V*>(base + (int64_t)(r0 + r) * ld + cc * VE);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) v[e] = 0;
+    }
+    *reinterpret_cast<V*>(s + r * LD + cc * VE) = v;
+  }
+}
+
+// bf16 fragment helpers (LD = 80)
+__device__ __forceinline__ bf16x8_t row_frag(const unsigned short* s, int rb, int ks, int lane) {
+  const unsigned short* p = s + (rb + (lane & 15)) * 80 + ks * 32 + (lane >> 4) * 8;
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(p));
+}
+__device__ __forceinline__ bf16x8_t tr_frag(const unsigned short* s, int cb, int ks, int lane) {
+  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const unsigned short* a0 = s + (ks * 32 + 4 * g + q) * 80 + cb + 4 * p;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(a0 + 16 * 80));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+// registers of a 16x16 f32 accumulator pair (sub-tiles 2ks, 2ks+1) -> bf16 B/A fragment
+__device__ __forceinline__ bf16x8_t pack_pair(const f32x4& x, const f32x4& y) {
+  u16x8 v = {f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3]),
+             f2bf(y[0]), f2bf(y[1]), f2bf(y[2]), f2bf(y[3])};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+// load a row fragment (16 rows at r0, lane row i, 8 contiguous cols at ks*32+8g) from global
+__device__ __forceinline__ bf16x8_t glob_row_frag(const unsigned short* base, int64_t ld, int r,
+                                                  int T, int ks, int lane) {
+  u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r < T) v = *reinterpret_cast<const u16x8*>(base + (int64_t)r * ld + ks * 32 + (lane >> 4) * 8);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <typename TI>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ============================================================================================
+// forward
+// ============================================================================================
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int LD = ACfg<TI>::LD;
+  __shared__ __attribute__((aligned(16))) TI sK[QT * LD];
+  __shared__ __attribute__((aligned(16))) TI sV[QT * LD];
+  __shared__ float sBias[QT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const int h = blockIdx.y, p = blockIdx.z;
+  const int q0 = blockIdx.x * QT + wave * 16;
+  const int T = a.T;
+  const TI* base = reinterpret_cast<const TI*>(a.qkv) + (int64_t)p * T * a.ld_qkv;
+  const TI* Qb = base + a.q_off + h * HD;
+  const TI* Kb = base + a.k_off + h * HD;
+  const TI* Vb = base + a.v_off + h * HD;
+  const float* kb_bias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+
+  f32x4 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = NEG, l = 0.f;
+
+  // Q fragments (B operand of S^T = K Q^T): lane (g,i) -> Q[q0+i][...]
+  bf16x8_t qf[2];
+  float qs[16];
+  if constexpr (sizeof(TI) == 2) {
+    qf[0] = glob_row_frag((const unsigned short*)Qb, a.ld_qkv, q0 + i, T, 0, lane);
+    qf[1] = glob_row_frag((const unsigned short*)Qb, a.ld_qkv, q0 + i, T, 1, lane);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+      qs[kk] = (q0 + i < T) ? ((const float*)Qb)[(int64_t)(q0 + i) * a.ld_qkv + kk * 4 + g] : 0.f;
+  }
+
+  const int nkt = (T + QT - 1) / QT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * QT;
+    stage_tile<TI>(sK, Kb, a.ld_qkv, k0, T, tid);
+    stage_tile<TI>(sV, Vb, a.ld_qkv, k0, T, tid);
+    if (tid < QT) {
+      int key = k0 + tid;
+      sBias[tid] = key < T ? (kb_bias ? kb_bias[key] : 0.f) : NEG;
+    }
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          s[kb] = mfma16<TI>(row_frag((const unsigned short*)sK, kb * 16, ks, lane), qf[ks], s[kb]);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+          s[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sK)[(kb * 16 + i) * LD + kk * 4 + g],
+                                                        qs[kk], s[kb], 0, 0, 0);
+      }
+    }
+    float mx = m;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = s[kb][r] * a.scale + sBias[kb * 16 + 4 * g + r];
+        s[kb][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float alpha = __expf(m - mx);
+    m = mx;
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float e = __expf(s[kb][r] - m);
+        s[kb][r] = e;
+        rs += e;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t pf = pack_pair(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          o[d] = mfma16<TI>(tr_frag((const unsigned short*)sV, d * 16, ks, lane), pf, o[d]);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            o[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                ((const float*)sV)[(kb * 16 + 4 * g + r) * LD + d * 16 + i], s[kb][r], o[d], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int q = q0 + i;
+  if (q < T) {
+    const float inv = 1.0f / l;
+    TI* op = reinterpret_cast<TI*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Elem<TI>::st(op + d * 16 + 4 * g + r, o[d][r] * inv);
+    if (g == 0) a.lse[((int64_t)p * a.heads + h) * T + q] = m + __logf(l);
+  }
+}
+
+// ============================================================================================
+// backward: delta = rowsum(dO * O)
+// ============================================================================================
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
+  // one wave per (p, t) row handles all heads: lane covers 64 dims of one head at a time
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t rows = (int64_t)a.P * a.T;
+  if (row >= rows) return;
+  const int p = row / a.T, t = row % a.T;
+  const TI* o = reinterpret_cast<const TI*>(a.out) + row * a.ld_out;
+  const TI* dO = reinterpret_cast<const TI*>(a.dout) + row * a.ld_dout;
+  for (int h = 0; h < a.heads; ++h) {
+    float v = Elem<TI>::ld(o + h * HD + lane) * Elem<TI>::ld(dO + h * HD + lane);
+    v = wave_sum(v);
+    if (lane == 0) a.delta[((int64_t)p * a.heads + h) * a.T + t] = v;
+  }
+}
+
+// ============================================================================================
+// backward: dK, dV (per 64-key tile; each wave owns 16 keys; queries swept through LDS)
+// ============================================================================================
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnArgs a) {
+  constexpr int LD = ACfg<TI>::LD;
+  __shared__ __attribute__((aligned(16))) TI sQ[QT * LD];
+  __shared__ __attribute__((aligned(16))) TI sdO[QT * LD];
+  __shared__ float sL[QT], sD[QT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const int h = blockIdx.y, p = blockIdx.z;
+  const int key0 = blockIdx.x * QT + wave * 16;
+  const int T = a.T;
+  const TI* base = reinterpret_cast<const TI*>(a.qkv) + (int64_t)p * T * a.ld_qkv;
+  const TI* Qb = base + a.q_off + h * HD;
+  const TI* Kb = base + a.k_off + h * HD;
+  const TI* Vb = base + a.v_off + h * HD;
+  const TI* dOb = reinterpret_cast<const TI*>(a.dout) + (int64_t)p * T * a.ld_dout + h * HD;
+  const float* lse = a.lse + ((int64_t)p * a.heads + h) * T;
+  const float* dl = a.delta + ((int64_t)p * a.heads + h) * T;
+  // this lane's key (lane i) bias
+  const int mykey = key0 + i;
+  const float kbias = mykey < T ? (a.key_bias ? a.key_bias[(int64_t)p * T + mykey] : 0.f) : NEG;
+
+  // K, V fragments in registers (B operand with key on the lane: B[k=d][col=key])
+  bf16x8_t kf[2], vf[2];
+  float ks_[16], vs_[16];
+  if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = glob_row_frag((const unsigned short*)Kb, a.ld_qkv, mykey, T, ks, lane);
+      vf[ks] = glob_row_frag((const unsigned short*)Vb, a.ld_qkv, mykey, T, ks, lane);
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      ks_[kk] = mykey < T ? ((const float*)Kb)[(int64_t)mykey * a.ld_qkv + kk * 4 + g] : 0.f;
+      vs_[kk] = mykey < T ? ((const float*)Vb)[(int64_t)mykey * a.ld_qkv + kk * 4 + g] : 0.f;
+    }
+  }
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    dk[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    dv[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  const int nqt = (T + QT - 1) / QT;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int qb0 = qt * QT;
+    stage_tile<TI>(sQ, Qb, a.ld_qkv, qb0, T, tid);
+    stage_tile<TI>(sdO, dOb, a.ld_dout, qb0, T, tid);
+    if (tid < QT) {
+      int q = qb0 + tid;
+      sL[tid] = q < T ? lse[q] : 1e30f;   // exp(s - 1e30) = 0 for padded queries
+      sD[tid] = q < T ? dl[q] : 0.f;
+    }
+    __syncthreads();
+    // S[q][key] and dP[q][key]: 4 query sub-tiles of 16 (rows 4g+r), key on the lane
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs) {
+      s[qs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dp[qs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s[qs] = mfma16<TI>(row_frag((const unsigned short*)sQ, qs * 16, ks, lane), kf[ks], s[qs]);
+          dp[qs] = mfma16<TI>(row_frag((const unsigned short*)sdO, qs * 16, ks, lane), vf[ks], dp[qs]);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+          s[qs] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sQ)[(qs * 16 + i) * LD + kk * 4 + g],
+                                                        ks_[kk], s[qs], 0, 0, 0);
+          dp[qs] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sdO)[(qs * 16 + i) * LD + kk * 4 + g],
+                                                         vs_[kk], dp[qs], 0, 0, 0);
+        }
+      }
+    }
+    // P = exp(S*scale + bias - lse[q]);  dS = P * (dP - D[q])
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int qi = qs * 16 + 4 * g + r;
+        float pv = __expf(s[qs][r] * a.scale + kbias - sL[qi]);
+        s[qs][r] = pv;
+        dp[qs][r] = pv * (dp[qs][r] - sD[qi]);
+      }
+    // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+    if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t pf = pack_pair(s[2 * ks], s[2 * ks + 1]);
+        bf16x8_t dsf = pack_pair(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          dv[d] = mfma16<TI>(tr_frag((const unsigned short*)sdO, d * 16, ks, lane), pf, dv[d]);
+          dk[d] = mfma16<TI>(tr_frag((const unsigned short*)sQ, d * 16, ks, lane), dsf, dk[d]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            int qi = qs * 16 + 4 * g + r;
+            dv[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sdO)[qi * LD + d * 16 + i],
+                                                          s[qs][r], dv[d], 0, 0, 0);
+            dk[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sQ)[qi * LD + d * 16 + i],
+                                                          dp[qs][r], dk[d], 0, 0, 0);
+          }
+    }
+    __syncthreads();
+  }
+  if (mykey < T) {
+    TI* dq = reinterpret_cast<TI*>(a.dqkv) + ((int64_t)p * T + mykey) * a.ld_dqkv;
+    TI* dkp = dq + a.k_off + h * HD;
+    TI* dvp = dq + a.v_off + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Elem<TI>::st(dkp + d * 16 + 4 * g + r, dk[d][r] * a.scale);
+        Elem<TI>::st(dvp + d * 16 + 4 * g + r, dv[d][r]);
+      }
+  }
+}
+
+// ============================================================================================
+// backward: dQ (per 64-query tile; each wave owns 16 queries; keys swept through LDS)
+// ============================================================================================
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_dq_kernel(AttnArgs a) {
+  constexpr int LD = ACfg<TI>::LD;
+  __shared__ __attribute__((aligned(16))) TI sK[QT * LD];
+  __shared__ __attribute__((aligned(16))) TI sV[QT * LD];
+  __shared__ float sBias[QT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const int h = blockIdx.y, p = blockIdx.z;
+  const int q0 = blockIdx.x * QT + wave * 16;
+  const int T = a.T;
+  const int myq = q0 + i;
+  const TI* base = reinterpret_cast<const TI*>(a.qkv) + (int64_t)p * T * a.ld_qkv;
+  const TI* Qb = base + a.q_off + h * HD;
+  const TI* Kb = base + a.k_off + h * HD;
+  const TI* Vb = base + a.v_off + h * HD;
+  const TI* dOb = reinterpret_cast<const TI*>(a.dout) + (int64_t)p * T * a.ld_dout + h * HD;
+  const float* kb_bias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+  const float L = myq < T ? a.lse[((int64_t)p * a.heads + h) * T + myq] : 1e30f;
+  const float D = myq < T ? a.delta[((int64_t)p * a.heads + h) * T + myq] : 0.f;
+
+  bf16x8_t qf[2], of[2];
+  float qs_[16], os_[16];
+  if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[ks] = glob_row_frag((const unsigned short*)Qb, a.ld_qkv, myq, T, ks, lane);
+      of[ks] = glob_row_frag((const unsigned short*)dOb, a.ld_dout, myq, T, ks, lane);
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      qs_[kk] = myq < T ? ((const float*)Qb)[(int64_t)myq * a.ld_qkv + kk * 4 + g] : 0.f;
+      os_[kk] = myq < T ? ((const float*)dOb)[(int64_t)myq * a.ld_dout + kk * 4 + g] : 0.f;
+    }
+  }
+  f32x4 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (T + QT - 1) / QT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * QT;
+    stage_tile<TI>(sK, Kb, a.ld_qkv, k0, T, tid);
+    stage_tile<TI>(sV, Vb, a.ld_qkv, k0, T, tid);
+    if (tid < QT) {
+      int key = k0 + tid;
+      sBias[tid] = key < T ? (kb_bias ? kb_bias[key] : 0.f) : NEG;
+    }
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dp[kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s[kb] = mfma16<TI>(row_frag((const unsigned short*)sK, kb * 16, ks, lane), qf[ks], s[kb]);
+          dp[kb] = mfma16<TI>(row_frag((const unsigned short*)sV, kb * 16, ks, lane), of[ks], dp[kb]);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+          s[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sK)[(kb * 16 + i) * LD + kk * 4 + g],
+                                                        qs_[kk], s[kb], 0, 0, 0);
+          dp[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(((const float*)sV)[(kb * 16 + i) * LD + kk * 4 + g],
+                                                         os_[kk], dp[kb], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = __expf(s[kb][r] * a.scale + sBias[kb * 16 + 4 * g + r] - L);
+        dp[kb][r] = pv * (dp[kb][r] - D);
+      }
+    if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t dsf = pack_pair(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          dq[d] = mfma16<TI>(tr_frag((const unsigned short*)sK, d * 16, ks, lane), dsf, dq[d]);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            dq[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                ((const float*)sK)[(kb * 16 + 4 * g + r) * LD + d * 16 + i], dp[kb][r], dq[d], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  if (myq < T) {
+    TI* dqp = reinterpret_cast<TI*>(a.dqkv) + ((int64_t)p * T + myq) * a.ld_dqkv + a.q_off + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Elem<TI>::st(dqp + d * 16 + 4 * g + r, dq[d][r] * a.scale);
+  }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+mmseq_status check_common(int P, int T, int heads, const void* qkv, int64_t ld, int64_t qo,
+                          int64_t ko, int64_t vo, mmseq_dtype dt) {
+  MMSEQ_REQUIRE(P >= 0 && T > 0 && heads > 0, "attn: bad sizes P=%d T=%d heads=%d", P, T, heads);
+  MMSEQ_REQUIRE(dt == MMSEQ_F32 || dt == MMSEQ_BF16, "attn: bad dtype");
+  const int ve = dt == MMSEQ_BF16 ? 8 : 4;
+  MMSEQ_REQUIRE(aligned16(qkv) && ld % ve == 0 && qo % ve == 0 && ko % ve == 0 && vo % ve == 0,
+                "attn: qkv must be 16-byte aligned with ld/offsets multiple of %d", ve);
+  MMSEQ_REQUIRE(qo + heads * 64 <= ld && ko + heads * 64 <= ld && vo + heads * 64 <= ld,
+                "attn: head slices exceed the row");
+  return MMSEQ_OK;
+}
+
+}  // namespace
+
+extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                       int64_t q_off, int64_t k_off, int64_t v_off,
+                                       const float* key_bias, float scale, void* out,
+                                       int64_t ld_out, float* lse, mmseq_dtype dtype,
+                                       mmseq_stream stream) {
+  mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
+  if (st) return st;
+  MMSEQ_REQUIRE(out && lse && ld_out >= heads * 64, "attn_fwd: bad out/lse");
+  if (P == 0) return MMSEQ_OK;
+  AttnArgs a = {};
+  a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
+  a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
+  a.o_w = out; a.ld_out = ld_out; a.lse = lse;
+  dim3 grid((T + QT - 1) / QT, heads, P);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MMSEQ_BF16)
+    hipLaunchKernelGGL(attn_fwd_kernel<unsigned short>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, s, a);
+  return mmseq_check_launch("attn_fwd");
+}
+
+extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                       int64_t q_off, int64_t k_off, int64_t v_off,
+                                       const float* key_bias, float scale, const void* out,
+                                       int64_t ld_out, const void* dout, int64_t ld_dout,
+                                       const float* lse, float* delta, void* dqkv,
+                                       int64_t ld_dqkv, mmseq_dtype dtype, mmseq_stream stream) {
+  mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
+  if (st) return st;
+  const int ve = dtype == MMSEQ_BF16 ? 8 : 4;
+  MMSEQ_REQUIRE(out && dout && lse && delta && dqkv, "attn_bwd: null buffer");
+  MMSEQ_REQUIRE(aligned16(dout) && ld_dout % ve == 0 && ld_dqkv >= ld_qkv - 0 && ld_dqkv % 1 == 0,
+                "attn_bwd: dout alignment");
+  if (P == 0) return MMSEQ_OK;
+  AttnArgs a = {};
+  a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
+  a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
+  a.out = out; a.ld_out = ld_out; a.dout = dout; a.ld_dout = ld_dout;
+  a.lse = const_cast<float*>(lse); a.delta = delta; a.dqkv = dqkv; a.ld_dqkv = ld_dqkv;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t rows = (int64_t)P * T;
+  dim3 gd((unsigned)((rows + 3) / 4));
+  dim3 grid((T + QT - 1) / QT, heads, P);
+  if (dtype == MMSEQ_BF16) {
+    hipLaunchKernelGGL(attn_delta_kernel<unsigned short>, gd, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_dkdv_kernel<unsigned short>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_dq_kernel<unsigned short>, grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(attn_delta_kernel<float>, gd, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_dkdv_kernel<float>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_dq_kernel<float>, grid, dim3(256), 0, s, a);
+  }
+  return mmseq_check_launch("attn_bwd");
+}

@@ -1,0 +1,93 @@
+// Shared device helpers for the mmseq HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mmseq.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+#define MMSEQ_LDS __attribute__((address_space(3)))
+
+// --- bf16 <-> f32 (round-to-nearest-even; NaN kept NaN via the hardware cvt) ---
+__device__ __forceinline__ float bf2f(unsigned short h) {
+  return __uint_as_float(((unsigned)h) << 16);
+}
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+// Generic element load/store for the two storage types used on the path.
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <> struct Elem<unsigned short> {
+  static __device__ __forceinline__ float ld(const unsigned short* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(unsigned short* p, float v) { *p = f2bf(v); }
+};
+
+// --- wave64 reductions ---
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// --- activations (reference sites in include/mmseq.h) ---
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case MMSEQ_ACT_GELU_ERF: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    case MMSEQ_ACT_QUICKGELU: return x / (1.0f + __expf(-1.702f * x));
+    case MMSEQ_ACT_TANH: return tanhf(x);
+    case MMSEQ_ACT_GELU_TANH: {
+      const float k = 0.79788456080286536f;  // sqrt(2/pi)
+      return 0.5f * x * (1.0f + tanhf(k * (x + 0.044715f * x * x * x)));
+    }
+    default: return x;
+  }
+}
+// d act / dx evaluated at the pre-activation x
+__device__ __forceinline__ float act_bwd(int act, float x) {
+  switch (act) {
+    case MMSEQ_ACT_GELU_ERF: {
+      float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+      float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+      return cdf + x * pdf;
+    }
+    case MMSEQ_ACT_QUICKGELU: {
+      float s = 1.0f / (1.0f + __expf(-1.702f * x));
+      return s + 1.702f * x * s * (1.0f - s);
+    }
+    case MMSEQ_ACT_TANH: {
+      float t = tanhf(x);
+      return 1.0f - t * t;
+    }
+    case MMSEQ_ACT_GELU_TANH: {
+      const float k = 0.79788456080286536f;
+      float u = k * (x + 0.044715f * x * x * x);
+      float t = tanhf(u);
+      return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k * (1.0f + 3.0f * 0.044715f * x * x);
+    }
+    default: return 1.0f;
+  }
+}
+
+// status plumbing shared by the ABI wrappers
+mmseq_status mmseq_set_error(mmseq_status code, const char* fmt, ...);
+mmseq_status mmseq_check_launch(const char* what);
+
+#define MMSEQ_REQUIRE(cond, ...) \
+  do { if (!(cond)) return mmseq_set_error(MMSEQ_EINVAL, __VA_ARGS__); } while (0)

@@ -1,0 +1,358 @@
+// MFMA GEMM for every Linear on the path (see include/mmseq.h: mmseq_gemm).
+//
+// Design (gfx950): 256-thread workgroups (4 waves, 2x2), 128x128 output tile, each wave a 64x64
+// sub-tile of 4x4 MFMA 16x16 tiles. bf16 operands use v_mfma_f32_16x16x32_bf16 (BK = 64),
+// fp32 operands the exact-fp32 v_mfma_f32_16x16x4_f32 (BK = 32, parity mode).
+// Two operand layouts only:
+//   NT (forward  Y = X W^T, dgrad dX = dY W with the bf16 W^T shadow): both operands
+//      K-contiguous -> LDS [rows][BK+pad], fragments by 16-byte ds_read_b128 row reads.
+//   TN (wgrad  dW = dY^T X): both operands M/N-contiguous -> LDS [BK][rows+pad], fragments by
+//      ds_read_b64_tr_b16 transposed reads; the k order inside a 32-step is permuted identically
+//      for both operands ({4g..4g+3} U {16+4g..16+4g+3} for lane group g) so every 32-lane half of
+//      a transposed read touches 8 distinct LDS rows spaced 72 dwords apart: conflict-free.
+// The MFMA is issued with the operands swapped (B-fragment as "A"), so each accumulator holds
+// C^T: lane (g = l>>4, i = l&15) owns C[m0+i][n0+4g .. n0+4g+3] -> 4 contiguous outputs per lane
+// for the fused epilogue (bias, activation / activation-backward, residual, accumulate).
+// Staging: global -> registers (16 B per lane per chunk, issued before the MFMA loop of the
+// previous tile) -> LDS after the barrier (the async-STAGE split of the guide, T14).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, NT_THREADS = 256;
+
+template <typename TI> struct Cfg;
+template <> struct Cfg<unsigned short> {  // bf16
+  static constexpr int BK = 64, VE = 8;
+  static constexpr int PADK = 16;  // NT row = 80 elems = 160 B (conflict-free b128 row reads)
+  static constexpr int PADM = 16;  // TN row = 144 elems = 288 B = 72 dwords (== 8 mod 64)
+};
+template <> struct Cfg<float> {
+  static constexpr int BK = 32, VE = 4;
+  static constexpr int PADK = 4;   // NT row = 36 floats
+  static constexpr int PADM = 4;   // TN row = 132 floats
+};
+
+struct GemmArgs {
+  int M, N, K;
+  const void* A; int64_t lda, sA;
+  const void* B; int64_t ldb, sB;
+  void* C; int64_t ldc, sC;
+  const float* bias; int act; void* aux; const void* dact; const void* resid; int64_t ldr, sR;
+  float alpha; int accumulate; int vec_ok; int vec_c;
+};
+
+template <typename TI, bool TRANS>
+struct Tile {
+  static constexpr int BK = Cfg<TI>::BK, VE = Cfg<TI>::VE;
+  // NT: [rows][BK+PADK]; TN: [BK][rows+PADM]
+  static constexpr int LD = TRANS ? (BM + Cfg<TI>::PADM) : (BK + Cfg<TI>::PADK);
+  static constexpr int ELEMS = TRANS ? BK * LD : BM * LD;
+  static constexpr int CHUNKS_PER_ROW = TRANS ? BM / VE : BK / VE;
+  static constexpr int NCHUNK = (BM * BK / VE) / NT_THREADS;  // = 4
+};
+
+template <typename TI> struct Vec16;
+template <> struct Vec16<unsigned short> { typedef u16x8 T; };
+template <> struct Vec16<float> { typedef f32x4 T; };
+
+// Load chunk `c` of this thread for one operand tile into registers (zero-fill out of range).
+// rows_lim = M (or N) bound for the "row" (m/n) index; K bound for k.
+template <typename TI, bool TRANS>
+__device__ __forceinline__ typename Vec16<TI>::T load_chunk(const TI* __restrict__ base, int64_t ld,
+                                                            int row0, int k0, int c, int tid,
+                                                            int rows_lim, int K, bool vec_ok) {
+  typedef Tile<TI, TRANS> Tl;
+  typedef typename Vec16<TI>::T V;
+  constexpr int VE = Tl::VE;
+  int L = c * NT_THREADS + tid;
+  int r = L / Tl::CHUNKS_PER_ROW, cc = L % Tl::CHUNKS_PER_ROW;
+  V out;
+  if (!TRANS) {
+    int row = row0 + r, k = k0 + cc * VE;
+    const TI* p = base + (int64_t)row * ld + k;
+    if (row < rows_lim && vec_ok && k + VE <= K) {
+      out = *reinterpret_cast<const V*>(p);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        TI v = 0;
+        if (row < rows_lim && k + e < K) v = p[e];
+        out[e] = v;
+      }
+    }
+  } else {
+    int k = k0 + r, col = row0 + cc * VE;
+    const TI* p = base + (int64_t)k * ld + col;
+    if (k < K && vec_ok && col + VE <= rows_lim) {
+      out = *reinterpret_cast<const V*>(p);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        TI v = 0;
+        if (k < K && col + e < rows_lim) v = p[e];
+        out[e] = v;
+      }
+    }
+  }
+  return out;
+}
+
+template <typename TI, bool TRANS>
+__device__ __forceinline__ void store_chunk(TI* __restrict__ s, typename Vec16<TI>::T v, int c,
+                                            int tid) {
+  typedef Tile<TI, TRANS> Tl;
+  int L = c * NT_THREADS + tid;
+  int r = L / Tl::CHUNKS_PER_ROW, cc = L % Tl::CHUNKS_PER_ROW;
+  *reinterpret_cast<typename Vec16<TI>::T*>(s + r * Tl::LD + cc * Tl::VE) = v;
+}
+
+// ---- fragment reads ------------------------------------------------------------------------
+// bf16 NT: lane (g, i) -> 8 contiguous k of row (rb + i) at k = ks*32 + 8g.
+__device__ __forceinline__ bf16x8_t frag_nt_bf16(const unsigned short* s, int rb, int ks, int lane) {
+  typedef Tile<unsigned short, false> Tl;
+  const unsigned short* p = s + (rb + (lane & 15)) * Tl::LD + ks * 32 + (lane >> 4) * 8;
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(p));
+}
+// bf16 TN: two ds_read_b64_tr_b16; lane (g, i=4q+p) supplies row (ks*32 + 4g + q [+16]),
+// columns rb + 4p .. +3, and receives column rb + i of the 4 rows.
+__device__ __forceinline__ bf16x8_t frag_tn_bf16(const unsigned short* s, int rb, int ks, int lane) {
+  typedef Tile<unsigned short, true> Tl;
+  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const unsigned short* a0 = s + (ks * 32 + 4 * g + q) * Tl::LD + rb + 4 * p;
+  const unsigned short* a1 = a0 + 16 * Tl::LD;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(a1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <typename TO>
+__device__ __forceinline__ void epilogue4(const GemmArgs& a, TO* __restrict__ C, const TO* resid,
+                                          TO* aux, const TO* dact, int m, int n, const float* acc) {
+  if (m >= a.M || n >= a.N) return;
+  float v[4];
+  bool full = (n + 3 < a.N);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r] = acc[r] * a.alpha;
+    if (a.bias && n + r < a.N) v[r] += a.bias[n + r];
+  }
+  TO* cp = C + (int64_t)m * a.ldc + n;
+  if (dact) {
+    const TO* dp = dact + (int64_t)m * a.ldc + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) v[r] *= act_bwd(a.act, Elem<TO>::ld(dp + r));
+  } else if (a.act) {
+    TO* ap = aux ? aux + (int64_t)m * a.ldc + n : nullptr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r < a.N) {
+        if (ap) Elem<TO>::st(ap + r, v[r]);
+        v[r] = act_fwd(a.act, v[r]);
+      }
+    }
+  }
+  if (resid) {
+    const TO* rp = resid + (int64_t)m * a.ldr + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) v[r] += Elem<TO>::ld(rp + r);
+  }
+  if (a.accumulate) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) v[r] += Elem<TO>::ld(cp + r);
+  }
+  if (full && a.vec_c) {
+    if (sizeof(TO) == 2) {
+      u16x4 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      *reinterpret_cast<u16x4*>(cp) = o;
+    } else {
+      f32x4 o = {v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(cp) = o;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) Elem<TO>::st(cp + r, v[r]);
+  }
+}
+
+template <typename TI, typename TO, bool TRANS>
+__global__ __launch_bounds__(NT_THREADS) void gemm_kernel(GemmArgs a) {
+  typedef Tile<TI, TRANS> Tl;
+  typedef typename Vec16<TI>::T V;
+  constexpr int BK = Tl::BK;
+  __shared__ __attribute__((aligned(16))) TI smem[2 * Tl::ELEMS];
+  TI* sA = smem;
+  TI* sB = smem + Tl::ELEMS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, b = blockIdx.z;
+  const TI* A = reinterpret_cast<const TI*>(a.A) + (int64_t)b * a.sA;
+  const TI* B = reinterpret_cast<const TI*>(a.B) + (int64_t)b * a.sB;
+  const bool vec = a.vec_ok;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  V ra[Tl::NCHUNK], rb[Tl::NCHUNK];
+  const int nk = (a.K + BK - 1) / BK;
+#pragma unroll
+  for (int c = 0; c < Tl::NCHUNK; ++c) {
+    ra[c] = load_chunk<TI, TRANS>(A, a.lda, m0, 0, c, tid, a.M, a.K, vec);
+    rb[c] = load_chunk<TI, TRANS>(B, a.ldb, n0, 0, c, tid, a.N, a.K, vec);
+  }
+#pragma unroll
+  for (int c = 0; c < Tl::NCHUNK; ++c) {
+    store_chunk<TI, TRANS>(sA, ra[c], c, tid);
+    store_chunk<TI, TRANS>(sB, rb[c], c, tid);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+#pragma unroll
+      for (int c = 0; c < Tl::NCHUNK; ++c) {
+        ra[c] = load_chunk<TI, TRANS>(A, a.lda, m0, (kt + 1) * BK, c, tid, a.M, a.K, vec);
+        rb[c] = load_chunk<TI, TRANS>(B, a.ldb, n0, (kt + 1) * BK, c, tid, a.N, a.K, vec);
+      }
+    }
+    if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8_t fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (TRANS) {
+            fa[i] = frag_tn_bf16((const unsigned short*)sA, wr * 64 + i * 16, ks, lane);
+            fb[i] = frag_tn_bf16((const unsigned short*)sB, wc * 64 + i * 16, ks, lane);
+          } else {
+            fa[i] = frag_nt_bf16((const unsigned short*)sA, wr * 64 + i * 16, ks, lane);
+            fb[i] = frag_nt_bf16((const unsigned short*)sB, wc * 64 + i * 16, ks, lane);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const int g = lane >> 4, ii = lane & 15;
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        float fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (TRANS) {
+            fa[i] = ((const float*)sA)[(kk + g) * Tl::LD + wr * 64 + i * 16 + ii];
+            fb[i] = ((const float*)sB)[(kk + g) * Tl::LD + wc * 64 + i * 16 + ii];
+          } else {
+            fa[i] = ((const float*)sA)[(wr * 64 + i * 16 + ii) * Tl::LD + kk + g];
+            fb[i] = ((const float*)sB)[(wc * 64 + i * 16 + ii) * Tl::LD + kk + g];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int c = 0; c < Tl::NCHUNK; ++c) {
+        store_chunk<TI, TRANS>(sA, ra[c], c, tid);
+        store_chunk<TI, TRANS>(sB, rb[c], c, tid);
+      }
+      __syncthreads();
+    }
+  }
+
+  TO* C = reinterpret_cast<TO*>(a.C) + (int64_t)b * a.sC;
+  const TO* resid = a.resid ? reinterpret_cast<const TO*>(a.resid) + (int64_t)b * a.sR : nullptr;
+  TO* aux = a.aux ? reinterpret_cast<TO*>(a.aux) + (int64_t)b * a.sC : nullptr;
+  const TO* dact = a.dact ? reinterpret_cast<const TO*>(a.dact) + (int64_t)b * a.sC : nullptr;
+  const int g = lane >> 4, ii = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m = m0 + wr * 64 + i * 16 + ii;
+      int n = n0 + wc * 64 + j * 16 + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epilogue4<TO>(a, C, resid, aux, dact, m, n, v);
+    }
+}
+
+template <typename TI, typename TO>
+hipError_t launch(int trans, const GemmArgs& a, int batch, hipStream_t s) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch);
+  if (trans)
+    hipLaunchKernelGGL((gemm_kernel<TI, TO, true>), grid, dim3(NT_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<TI, TO, false>), grid, dim3(NT_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+
+inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, const void* A,
+                                   int64_t lda, int64_t strideA, const void* B, int64_t ldb,
+                                   int64_t strideB, void* C, int64_t ldc, int64_t strideC,
+                                   const float* bias, int act, void* aux_out, const void* dact_aux,
+                                   const void* resid, int64_t ldr, int64_t strideR, float alpha,
+                                   int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
+                                   mmseq_stream stream) {
+  MMSEQ_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes M=%d N=%d K=%d b=%d",
+                M, N, K, batch);
+  MMSEQ_REQUIRE(A && B && C, "gemm: null operand");
+  MMSEQ_REQUIRE(act >= 0 && act <= 4, "gemm: bad act %d", act);
+  MMSEQ_REQUIRE(!(aux_out && dact_aux), "gemm: aux_out and dact_aux are exclusive");
+  MMSEQ_REQUIRE(in_dtype == MMSEQ_F32 || in_dtype == MMSEQ_BF16, "gemm: bad in dtype");
+  MMSEQ_REQUIRE(out_dtype == MMSEQ_F32 || out_dtype == MMSEQ_BF16, "gemm: bad out dtype");
+  if (!trans) {
+    MMSEQ_REQUIRE(lda >= K && ldb >= K && ldc >= N, "gemm NT: ld too small");
+  } else {
+    MMSEQ_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gemm TN: ld too small");
+  }
+  if (M == 0 || N == 0) return MMSEQ_OK;
+  GemmArgs a;
+  a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = lda; a.sA = strideA;
+  a.B = B; a.ldb = ldb; a.sB = strideB;
+  a.C = C; a.ldc = ldc; a.sC = strideC;
+  a.bias = bias; a.act = act; a.aux = aux_out; a.dact = dact_aux;
+  a.resid = resid; a.ldr = resid ? ldr : 0; a.sR = strideR;
+  a.alpha = alpha; a.accumulate = accumulate;
+  const int ve = in_dtype == MMSEQ_BF16 ? 8 : 4;
+  a.vec_ok = al16(A) && al16(B) && lda % ve == 0 && ldb % ve == 0 && strideA % ve == 0 &&
+             strideB % ve == 0;
+  const int vc = 4;
+  const int esz = out_dtype == MMSEQ_BF16 ? 2 : 4;
+  a.vec_c = ((uintptr_t)C % (vc * esz) == 0) && ldc % vc == 0 && strideC % vc == 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e;
+  if (in_dtype == MMSEQ_BF16 && out_dtype == MMSEQ_BF16)
+    e = launch<unsigned short, unsigned short>(trans, a, batch, s);
+  else if (in_dtype == MMSEQ_BF16 && out_dtype == MMSEQ_F32)
+    e = launch<unsigned short, float>(trans, a, batch, s);
+  else if (in_dtype == MMSEQ_F32 && out_dtype == MMSEQ_F32)
+    e = launch<float, float>(trans, a, batch, s);
+  else
+    e = launch<float, unsigned short>(trans, a, batch, s);
+  if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm launch: %s", hipGetErrorString(e));
+  return MMSEQ_OK;
+}

@@ -1,0 +1,413 @@
+// BERSON head kernels (models/berson/modeling_bert.py, neural.py): span pooling of the pair
+// encoder output, the pointer-network scoring + masked log-softmax + NLL, and the small
+// multi-head attention of the inter-sentence encoder. All fp32 compute; no host loops, no
+// device->host syncs (the reference does 2P .cpu() syncs + ~6P scalar index_put per step here).
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+  // 256 threads -> 4 waves
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  float r = is_max ? fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3])) : sh[0] + sh[1] + sh[2] + sh[3];
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// pointer scoring (modeling_bert.py:1083-1142)
+// ---------------------------------------------------------------------------------------------
+constexpr int MAXN = 32;
+
+__global__ __launch_bounds__(256) void pointer_fwd_kernel(int B, int N, int H,
+                                                          const float* __restrict__ q,
+                                                          const float* __restrict__ key,
+                                                          const float* __restrict__ okey,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ wbias,
+                                                          const uint8_t* __restrict__ pointed,
+                                                          const int64_t* __restrict__ tgt_len,
+                                                          const int64_t* __restrict__ target,
+                                                          float* __restrict__ logp,
+                                                          float* __restrict__ nll) {
+  __shared__ float e[MAXN];
+  const int b = blockIdx.x / N, t = blockIdx.x % N;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* qr = q + ((int64_t)b * N + t) * H;
+  const int L = (int)tgt_len[b];
+  for (int j = wave; j < N; j += 4) {
+    const float* kr = key + (((int64_t)b * N + t) * N + j) * H;
+    const float* orow = okey + ((int64_t)b * N + j) * H;
+    float s = 0.f;
+    for (int h = lane; h < H; h += 64) s += w[h] * tanhf(qr[h] + kr[h] + orow[h]);
+    s = wave_sum(s);
+    if (lane == 0) {
+      float v = s + (wbias ? wbias[0] : 0.f);
+      if (pointed[((int64_t)b * N + t) * N + j] != 0 || j >= L) v = -1e9f;  // :1112-1113
+      e[j] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mx = -INFINITY;
+    for (int j = 0; j < N; ++j) mx = fmaxf(mx, e[j]);
+    float s = 0.f;
+    for (int j = 0; j < N; ++j) s += expf(e[j] - mx);
+    const float lse = mx + logf(s);
+    for (int j = 0; j < N; ++j) logp[((int64_t)b * N + t) * N + j] = e[j] - lse;
+    const int tg = (int)target[(int64_t)b * N + t];
+    nll[(int64_t)b * N + t] = t < L ? -(e[tg] - lse) : 0.f;  // :1126-1135
+  }
+}
+
+__global__ __launch_bounds__(256) void pointer_bwd_kernel(int B, int N, int H,
+                                                          const float* __restrict__ q,
+                                                          const float* __restrict__ key,
+                                                          const float* __restrict__ okey,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ logp,
+                                                          const uint8_t* __restrict__ pointed,
+                                                          const int64_t* __restrict__ tgt_len,
+                                                          const int64_t* __restrict__ target,
+                                                          const float* __restrict__ dnll,
+                                                          float* __restrict__ dq,
+                                                          float* __restrict__ dkey,
+                                                          float* __restrict__ dokey,
+                                                          float* __restrict__ dw,
+                                                          float* __restrict__ dwb) {
+  __shared__ float de[MAXN];
+  const int b = blockIdx.x / N, t = blockIdx.x % N;
+  const int L = (int)tgt_len[b];
+  if (threadIdx.x < N) {
+    const int j = threadIdx.x;
+    const int tg = (int)target[(int64_t)b * N + t];
+    float g = t < L ? dnll[(int64_t)b * N + t] : 0.f;
+    float sm = expf(logp[((int64_t)b * N + t) * N + j]);
+    // masked entries were overwritten with -1e9 (masked_fill_): no gradient flows through them
+    const bool masked = pointed[((int64_t)b * N + t) * N + j] != 0 || j >= L;
+    de[j] = masked ? 0.f : g * (sm - (j == tg ? 1.f : 0.f));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int j = 0; j < N; ++j) s += de[j];
+    atomicAdd(dwb, s);
+  }
+  const float* qr = q + ((int64_t)b * N + t) * H;
+  for (int h = threadIdx.x; h < H; h += 256) {
+    float dqh = 0.f, dwh = 0.f;
+    const float wh = w[h], qh = qr[h];
+    for (int j = 0; j < N; ++j) {
+      const int64_t kidx = (((int64_t)b * N + t) * N + j) * H + h;
+      const int64_t oidx = ((int64_t)b * N + j) * H + h;
+      float th = tanhf(qh + key[kidx] + okey[oidx]);
+      float d = de[j] * wh * (1.f - th * th);
+      dkey[kidx] = d;
+      dqh += d;
+      dwh += de[j] * th;
+      atomicAdd(dokey + oidx, d);
+    }
+    dq[((int64_t)b * N + t) * H + h] = dqh;
+    atomicAdd(dw + h, dwh);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// HierarchicalAttention span pooling (modeling_bert.py:703-741)
+// ---------------------------------------------------------------------------------------------
+constexpr int MAXLT = 1024;
+
+__device__ __forceinline__ bool in_span(int s, int t, int s0, int s1) {
+  return s == 0 ? (t >= 1 && t <= s0) : (t > s0 && t <= s1);  // :711-712
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void span_fwd_kernel(int P, int Lt, int H, const T* __restrict__ top,
+                                                       int64_t ld_pair, const float* __restrict__ score,
+                                                       const int64_t* __restrict__ sep,
+                                                       float* __restrict__ probs,
+                                                       float* __restrict__ mix) {
+  __shared__ float pr[2][MAXLT];
+  __shared__ float red[4];
+  const int p = blockIdx.x;
+  const int s0 = (int)sep[2 * p], s1 = (int)sep[2 * p + 1];
+  for (int s = 0; s < 2; ++s) {
+    float mx = -INFINITY;
+    for (int t = threadIdx.x; t < Lt; t += 256) {
+      // (1-m)*-10000 + m*score, exactly as :722-731
+      float a = in_span(s, t, s0, s1) ? score[(int64_t)p * Lt + t] : -10000.0f;
+      pr[s][t] = a;
+      mx = fmaxf(mx, a);
+    }
+    mx = block_reduce(mx, red, true);
+    float sum = 0.f;
+    for (int t = threadIdx.x; t < Lt; t += 256) {
+      float e = expf(pr[s][t] - mx);
+      pr[s][t] = e;
+      sum += e;
+    }
+    sum = block_reduce(sum, red, false);
+    const float inv = 1.f / sum;
+    for (int t = threadIdx.x; t < Lt; t += 256) {
+      pr[s][t] *= inv;
+      probs[((int64_t)p * 2 + s) * Lt + t] = pr[s][t];
+    }
+  }
+  __syncthreads();
+  const T* tp = top + (int64_t)p * ld_pair;
+  for (int h = threadIdx.x; h < H; h += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int t = 0; t < Lt; ++t) {
+      float v = Elem<T>::ld(tp + (int64_t)t * H + h);
+      a0 += pr[0][t] * v;
+      a1 += pr[1][t] * v;
+    }
+    mix[((int64_t)p * 2 + 0) * H + h] = a0;
+    mix[((int64_t)p * 2 + 1) * H + h] = a1;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void span_bwd_kernel(int P, int Lt, int H, const T* __restrict__ top,
+                                                       int64_t ld_pair, const float* __restrict__ probs,
+                                                       const int64_t* __restrict__ sep,
+                                                       const float* __restrict__ dmix,
+                                                       float* __restrict__ dscore,
+                                                       T* __restrict__ dtop) {
+  __shared__ float dpr[2][MAXLT];
+  __shared__ float red[4];
+  const int p = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s0 = (int)sep[2 * p], s1 = (int)sep[2 * p + 1];
+  const T* tp = top + (int64_t)p * ld_pair;
+  const float* dm0 = dmix + ((int64_t)p * 2 + 0) * H;
+  const float* dm1 = dmix + ((int64_t)p * 2 + 1) * H;
+  for (int t = wave; t < Lt; t += 4) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int h = lane; h < H; h += 64) {
+      float v = Elem<T>::ld(tp + (int64_t)t * H + h);
+      a0 += dm0[h] * v;
+      a1 += dm1[h] * v;
+    }
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    if (lane == 0) {
+      dpr[0][t] = a0;
+      dpr[1][t] = a1;
+    }
+  }
+  __syncthreads();
+  const float* pr0 = probs + ((int64_t)p * 2 + 0) * Lt;
+  const float* pr1 = probs + ((int64_t)p * 2 + 1) * Lt;
+  float c0 = 0.f, c1 = 0.f;
+  for (int t = threadIdx.x; t < Lt; t += 256) {
+    c0 += pr0[t] * dpr[0][t];
+    c1 += pr1[t] * dpr[1][t];
+  }
+  c0 = block_reduce(c0, red, false);
+  c1 = block_reduce(c1, red, false);
+  for (int t = threadIdx.x; t < Lt; t += 256) {
+    float d = 0.f;
+    if (in_span(0, t, s0, s1)) d += pr0[t] * (dpr[0][t] - c0);
+    if (in_span(1, t, s0, s1)) d += pr1[t] * (dpr[1][t] - c1);
+    dscore[(int64_t)p * Lt + t] = d;
+  }
+  T* dtp = dtop + (int64_t)p * ld_pair;
+  for (int t = 0; t < Lt; ++t) {
+    const float w0 = pr0[t], w1 = pr1[t];
+    for (int h = threadIdx.x; h < H; h += 256) {
+      T* d = dtp + (int64_t)t * H + h;
+      Elem<T>::st(d, Elem<T>::ld(d) + w0 * dm0[h] + w1 * dm1[h]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// small MHA for the inter-sentence encoder (neural.py:98-235): one workgroup per (b, head)
+// ---------------------------------------------------------------------------------------------
+constexpr int SA_T = 64;
+
+__global__ __launch_bounds__(256) void small_attn_fwd_kernel(int B, int T, int heads, int d,
+                                                             const float* __restrict__ q,
+                                                             const float* __restrict__ k,
+                                                             const float* __restrict__ v,
+                                                             const float* __restrict__ kbias,
+                                                             float scale, float* __restrict__ out,
+                                                             float* __restrict__ probs) {
+  __shared__ float S[SA_T][SA_T + 1];
+  const int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int D = heads * d;
+  const float* qb = q + (int64_t)b * T * D + h * d;
+  const float* kb = k + (int64_t)b * T * D + h * d;
+  const float* vb = v + (int64_t)b * T * D + h * d;
+  for (int e = threadIdx.x; e < T * T; e += 256) {
+    int i = e / T, j = e % T;
+    float s = 0.f;
+    for (int c = 0; c < d; ++c) s += qb[(int64_t)i * D + c] * kb[(int64_t)j * D + c];
+    // neural.py:208-213: query pre-scaled by 1/sqrt(d), mask added as (1-m)*-10000
+    S[i][j] = s * scale + (kbias ? kbias[(int64_t)b * T + j] : 0.f);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < T; i += 256) {
+    float mx = -INFINITY;
+    for (int j = 0; j < T; ++j) mx = fmaxf(mx, S[i][j]);
+    float sum = 0.f;
+    for (int j = 0; j < T; ++j) {
+      float e = expf(S[i][j] - mx);
+      S[i][j] = e;
+      sum += e;
+    }
+    float inv = 1.f / sum;
+    for (int j = 0; j < T; ++j) {
+      S[i][j] *= inv;
+      probs[(((int64_t)b * heads + h) * T + i) * T + j] = S[i][j];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * d; e += 256) {
+    int i = e / d, c = e % d;
+    float s = 0.f;
+    for (int j = 0; j < T; ++j) s += S[i][j] * vb[(int64_t)j * D + c];
+    out[(int64_t)b * T * D + (int64_t)i * D + h * d + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void small_attn_bwd_kernel(int B, int T, int heads, int d,
+                                                             const float* __restrict__ q,
+                                                             const float* __restrict__ k,
+                                                             const float* __restrict__ v,
+                                                             const float* __restrict__ probs,
+                                                             const float* __restrict__ dout,
+                                                             float scale, float* __restrict__ dq,
+                                                             float* __restrict__ dk,
+                                                             float* __restrict__ dv) {
+  __shared__ float Pm[SA_T][SA_T + 1];
+  __shared__ float dS[SA_T][SA_T + 1];
+  const int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int D = heads * d;
+  const int64_t off = (int64_t)b * T * D + h * d;
+  for (int e = threadIdx.x; e < T * T; e += 256) {
+    int i = e / T, j = e % T;
+    Pm[i][j] = probs[(((int64_t)b * heads + h) * T + i) * T + j];
+    float s = 0.f;
+    for (int c = 0; c < d; ++c) s += dout[off + (int64_t)i * D + c] * v[off + (int64_t)j * D + c];
+    dS[i][j] = s;  // dP
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < T; i += 256) {
+    float c = 0.f;
+    for (int j = 0; j < T; ++j) c += Pm[i][j] * dS[i][j];
+    for (int j = 0; j < T; ++j) dS[i][j] = Pm[i][j] * (dS[i][j] - c);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * d; e += 256) {
+    int i = e / d, c = e % d;
+    float aq = 0.f, ak = 0.f, av = 0.f;
+    for (int j = 0; j < T; ++j) {
+      aq += dS[i][j] * k[off + (int64_t)j * D + c];
+      ak += dS[j][i] * q[off + (int64_t)j * D + c];
+      av += Pm[j][i] * dout[off + (int64_t)j * D + c];
+    }
+    dq[off + (int64_t)i * D + c] = aq * scale;
+    dk[off + (int64_t)i * D + c] = ak * scale;
+    dv[off + (int64_t)i * D + c] = av;
+  }
+}
+
+}  // namespace
+
+extern "C" mmseq_status mmseq_pointer_fwd(int B, int N, int H, const float* q, const float* key,
+                                          const float* okey, const float* w, const float* w_bias,
+                                          const uint8_t* pointed, const int64_t* tgt_len,
+                                          const int64_t* target, float* logp, float* nll,
+                                          mmseq_stream stream) {
+  MMSEQ_REQUIRE(B >= 0 && N > 0 && N <= MAXN && H > 0, "pointer: N must be in (0, %d]", MAXN);
+  MMSEQ_REQUIRE(q && key && okey && w && pointed && tgt_len && target && logp && nll,
+                "pointer_fwd: null buffer");
+  if (!B) return MMSEQ_OK;
+  hipLaunchKernelGGL(pointer_fwd_kernel, dim3(B * N), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, N, H, q, key, okey, w, w_bias,
+                     pointed, tgt_len, target, logp, nll);
+  return mmseq_check_launch("pointer_fwd");
+}
+
+extern "C" mmseq_status mmseq_pointer_bwd(int B, int N, int H, const float* q, const float* key,
+                                          const float* okey, const float* w, const float* logp,
+                                          const uint8_t* pointed, const int64_t* tgt_len, const int64_t* target,
+                                          const float* dnll, float* dq, float* dkey, float* dokey,
+                                          float* dw, float* dw_bias, mmseq_stream stream) {
+  MMSEQ_REQUIRE(B >= 0 && N > 0 && N <= MAXN && H > 0, "pointer_bwd: bad sizes");
+  MMSEQ_REQUIRE(q && key && okey && w && logp && pointed && tgt_len && target && dnll && dq &&
+                    dkey && dokey && dw && dw_bias,
+                "pointer_bwd: null buffer");
+  if (!B) return MMSEQ_OK;
+  hipLaunchKernelGGL(pointer_bwd_kernel, dim3(B * N), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, N, H, q, key, okey, w, logp,
+                     pointed, tgt_len, target, dnll, dq, dkey, dokey, dw, dw_bias);
+  return mmseq_check_launch("pointer_bwd");
+}
+
+extern "C" mmseq_status mmseq_span_pool_fwd(int P, int Lt, int H, const void* top,
+                                            int64_t ld_pair, const float* score,
+                                            const int64_t* sep, float* probs, float* mix,
+                                            mmseq_dtype dt, mmseq_stream stream) {
+  MMSEQ_REQUIRE(P >= 0 && Lt > 0 && Lt <= MAXLT && H > 0, "span_pool: Lt must be <= %d", MAXLT);
+  MMSEQ_REQUIRE(top && score && sep && probs && mix, "span_pool_fwd: null buffer");
+  if (!P) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dt == MMSEQ_F32)
+    hipLaunchKernelGGL(span_fwd_kernel<float>, dim3(P), dim3(256), 0, s, P, Lt, H,
+                       (const float*)top, ld_pair, score, sep, probs, mix);
+  else
+    hipLaunchKernelGGL(span_fwd_kernel<unsigned short>, dim3(P), dim3(256), 0, s, P, Lt, H,
+                       (const unsigned short*)top, ld_pair, score, sep, probs, mix);
+  return mmseq_check_launch("span_pool_fwd");
+}
+
+extern "C" mmseq_status mmseq_span_pool_bwd(int P, int Lt, int H, const void* top,
+                                            int64_t ld_pair, const float* probs,
+                                            const int64_t* sep, const float* dmix, float* dscore,
+                                            void* dtop, mmseq_dtype dt, mmseq_stream stream) {
+  MMSEQ_REQUIRE(P >= 0 && Lt > 0 && Lt <= MAXLT && H > 0, "span_pool_bwd: bad sizes");
+  MMSEQ_REQUIRE(top && probs && sep && dmix && dscore && dtop, "span_pool_bwd: null buffer");
+  if (!P) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dt == MMSEQ_F32)
+    hipLaunchKernelGGL(span_bwd_kernel<float>, dim3(P), dim3(256), 0, s, P, Lt, H,
+                       (const float*)top, ld_pair, probs, sep, dmix, dscore, (float*)dtop);
+  else
+    hipLaunchKernelGGL(span_bwd_kernel<unsigned short>, dim3(P), dim3(256), 0, s, P, Lt, H,
+                       (const unsigned short*)top, ld_pair, probs, sep, dmix, dscore,
+                       (unsigned short*)dtop);
+  return mmseq_check_launch("span_pool_bwd");
+}
+
+extern "C" mmseq_status mmseq_small_attn_fwd(int B, int T, int heads, int d, const float* q,
+                                             const float* k, const float* v,
+                                             const float* key_bias, float scale, float* out,
+                                             float* probs, mmseq_stream stream) {
+  MMSEQ_REQUIRE(B >= 0 && T > 0 && T <= SA_T && heads > 0 && d > 0, "small_attn: T must be <= %d",
+                SA_T);
+  MMSEQ_REQUIRE(q && k && v && out && probs, "small_attn_fwd: null buffer");
+  if (!B) return MMSEQ_OK;
+  hipLaunchKernelGGL(small_attn_fwd_kernel, dim3(B * heads), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, T, heads, d, q, k, v, key_bias,
+                     scale, out, probs);
+  return mmseq_check_launch("small_attn_fwd");
+}
+
+extern "C" mmseq_status mmseq_small_attn_bwd(int B, int T, int heads, int d, const float* q,
+                                             const float* k, const float* v, const float* probs,
+                                             const float* dout, float scale, float* dq, float* dk,
+                                             float* dv, mmseq_stream stream) {
+  MMSEQ_REQUIRE(B >= 0 && T > 0 && T <= SA_T && heads > 0 && d > 0, "small_attn_bwd: bad sizes");
+  MMSEQ_REQUIRE(q && k && v && probs && dout && dq && dk && dv, "small_attn_bwd: null buffer");
+  if (!B) return MMSEQ_OK;
+  hipLaunchKernelGGL(small_attn_bwd_kernel, dim3(B * heads), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, T, heads, d, q, k, v, probs, dout,
+                     scale, dq, dk, dv);
+  return mmseq_check_launch("small_attn_bwd");
+}

@@ -1,0 +1,207 @@
+// LayerNorm forward / backward with fp32 statistics (one wave64 per row, shuffle reductions).
+// Reference sites: lxrt/modeling.py:353,432,486,577 (BertLayerNorm eps 1e-12);
+// clip/model.py:190-196 (fp32 LayerNorm, eps 1e-5); berson/encoder.py:16,42, neural.py:25 (1e-6).
+// Rows are addressed through mmseq_rows (two-level strides) so the kernels can read / write the
+// text or the visual half of the joint [P][T][H] activation in place (the fused concat).
+#include "common.h"
+
+namespace {
+
+constexpr int MAXV = 16;  // cols <= 64 * 16 = 1024
+constexpr int RPB = 64;   // rows per workgroup in bwd (dgamma/dbeta partial granularity)
+
+__device__ __forceinline__ int64_t row_off(const mmseq_rows& l, int64_t r) {
+  return (r / l.rpb) * l.bstride + (r % l.rpb) * l.ld;
+}
+
+template <typename TX, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const TX* __restrict__ x,
+                                                     mmseq_rows xl, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     TY* __restrict__ y, mmseq_rows yl,
+                                                     float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const TX* xr = x + row_off(xl, r);
+  float v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    int c = j * 64 + lane;
+    v[j] = c < cols ? Elem<TX>::ld(xr + c) : 0.f;
+    s += v[j];
+  }
+  const float mu = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    int c = j * 64 + lane;
+    float d = c < cols ? v[j] - mu : 0.f;
+    q += d * d;
+  }
+  const float rs = rsqrtf(wave_sum(q) / cols + eps);
+  TY* yr = y + row_off(yl, r);
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    int c = j * 64 + lane;
+    if (c < cols) Elem<TY>::st(yr + c, (v[j] - mu) * rs * gamma[c] + beta[c]);
+  }
+  if (lane == 0) {
+    if (mean) mean[r] = mu;
+    if (rstd) rstd[r] = rs;
+  }
+}
+
+// dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres)
+// per-block partial dgamma / dbeta -> ws[block][2][cols]
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
+                                                     mmseq_rows dyl, const T* __restrict__ x,
+                                                     mmseq_rows xl, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma,
+                                                     T* __restrict__ dx, mmseq_rows dxl,
+                                                     const T* __restrict__ dres, mmseq_rows dresl,
+                                                     float* __restrict__ ws) {
+  __shared__ float red[4][2][1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[MAXV], pb[MAXV];
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) pg[j] = pb[j] = 0.f;
+  const int64_t rbeg = (int64_t)blockIdx.x * RPB;
+  for (int64_t r = rbeg + wave; r < rbeg + RPB && r < rows; r += 4) {
+    const T* xr = x + row_off(xl, r);
+    const T* dyr = dy + row_off(dyl, r);
+    const float mu = mean[r], rs = rstd[r];
+    float xh[MAXV], gdy[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      int c = j * 64 + lane;
+      if (c < cols) {
+        float xv = (Elem<T>::ld(xr + c) - mu) * rs;
+        float d = Elem<T>::ld(dyr + c);
+        xh[j] = xv;
+        gdy[j] = d * gamma[c];
+        pg[j] += d * xv;
+        pb[j] += d;
+        s1 += gdy[j];
+        s2 += gdy[j] * xv;
+      } else {
+        xh[j] = gdy[j] = 0.f;
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+    T* dxr = dx + row_off(dxl, r);
+    const T* drr = dres ? dres + row_off(dresl, r) : nullptr;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      int c = j * 64 + lane;
+      if (c < cols) {
+        float v = rs * (gdy[j] - s1 - xh[j] * s2);
+        if (drr) v += Elem<T>::ld(drr + c);
+        Elem<T>::st(dxr + c, v);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    int c = j * 64 + lane;
+    if (c < cols) {
+      red[wave][0][c] = pg[j];
+      red[wave][1][c] = pb[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    float g = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    float b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    ws[((int64_t)blockIdx.x * 2 + 0) * cols + c] = g;
+    ws[((int64_t)blockIdx.x * 2 + 1) * cols + c] = b;
+  }
+}
+
+// sum ws[nb][2][cols] over nb in a fixed order -> dgamma, dbeta (+=)
+__global__ __launch_bounds__(256) void ln_reduce_kernel(int nb, int cols, const float* __restrict__ ws,
+                                                        float* __restrict__ dg,
+                                                        float* __restrict__ db) {
+  // grid.x = ceil(2*cols / 64); each wave handles one (which, col) pair per lane-strided loop
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int idx = blockIdx.x * 64 + lane;  // 0 .. 2*cols-1
+  const int which = idx / cols, c = idx % cols;
+  float s = 0.f;
+  if (idx < 2 * cols)
+    for (int b = wave; b < nb; b += 4) s += ws[((int64_t)b * 2 + which) * cols + c];
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && idx < 2 * cols) {
+    float t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    float* dst = which == 0 ? dg : db;
+    if (dst) dst[c] += t;
+  }
+}
+
+}  // namespace
+
+mmseq_status ln_reduce_partials(int nb, int cols, const float* ws, float* dg, float* db,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(ln_reduce_kernel, dim3((2 * cols + 63) / 64), dim3(256), 0, s, nb, cols, ws,
+                     dg, db);
+  return mmseq_check_launch("ln_reduce");
+}
+
+extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, mmseq_rows xl,
+                                            const float* gamma, const float* beta, float eps,
+                                            void* y, mmseq_rows yl, float* mean, float* rstd,
+                                            mmseq_dtype xd, mmseq_dtype yd, mmseq_stream stream) {
+  MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 1024, "layernorm: cols must be in (0, 1024]");
+  MMSEQ_REQUIRE(x && y && gamma && beta, "layernorm: null buffer");
+  MMSEQ_REQUIRE(xl.rpb > 0 && yl.rpb > 0, "layernorm: rpb must be > 0");
+  if (rows == 0) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((rows + 3) / 4);
+#define LNF(TX, TY) \
+  hipLaunchKernelGGL((ln_fwd_kernel<TX, TY>), grid, dim3(256), 0, s, rows, cols, (const TX*)x, xl, \
+                     gamma, beta, eps, (TY*)y, yl, mean, rstd)
+  if (xd == MMSEQ_F32 && yd == MMSEQ_F32) LNF(float, float);
+  else if (xd == MMSEQ_F32 && yd == MMSEQ_BF16) LNF(float, unsigned short);
+  else if (xd == MMSEQ_BF16 && yd == MMSEQ_F32) LNF(unsigned short, float);
+  else LNF(unsigned short, unsigned short);
+#undef LNF
+  return mmseq_check_launch("layernorm_fwd");
+}
+
+extern "C" int64_t mmseq_layernorm_bwd_workspace(int rows, int cols) {
+  return (int64_t)((rows + RPB - 1) / RPB) * 2 * cols;
+}
+
+extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                            const void* x, mmseq_rows xl, const float* mean,
+                                            const float* rstd, const float* gamma, void* dx,
+                                            mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                            float* dgamma, float* dbeta, float* workspace,
+                                            mmseq_dtype dtype, mmseq_stream stream) {
+  MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 1024, "layernorm_bwd: cols must be in (0, 1024]");
+  MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "layernorm_bwd: null buffer");
+  if (rows == 0) return MMSEQ_OK;
+  if (!dres) dresl = dxl;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = (rows + RPB - 1) / RPB;
+  if (dtype == MMSEQ_F32)
+    hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(nb), dim3(256), 0, s, rows, cols,
+                       (const float*)dy, dyl, (const float*)x, xl, mean, rstd, gamma, (float*)dx,
+                       dxl, (const float*)dres, dresl, workspace);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<unsigned short>), dim3(nb), dim3(256), 0, s, rows, cols,
+                       (const unsigned short*)dy, dyl, (const unsigned short*)x, xl, mean, rstd,
+                       gamma, (unsigned short*)dx, dxl, (const unsigned short*)dres, dresl,
+                       workspace);
+  mmseq_status st = mmseq_check_launch("layernorm_bwd");
+  if (st) return st;
+  if (dgamma || dbeta) return ln_reduce_partials(nb, cols, workspace, dgamma, dbeta, s);
+  return MMSEQ_OK;
+}

@@ -1,0 +1,466 @@
+"""Autograd Functions over the HIP C ABI.
+
+Layer-level Functions (ViT block, BERT layer, stem, projection, joint input) own their forward
+AND backward explicitly: they decide what is saved (flash attention saves LSE, not T x T
+probabilities), fuse the residual adds into GEMM epilogues / LayerNorm backward, and write
+parameter gradients straight into the flat fp32 grad buffer of the ParamStore with accumulating
+wgrad GEMMs (so gradient accumulation over micro-batches is free and the all-reduce can start on
+a contiguous slice as soon as a layer's backward finishes). Autograd only sequences the layers:
+each Function takes an `anchor` tensor that requires grad so the graph is recorded, and returns
+None for it.
+"""
+import math
+
+import torch
+
+from . import _native as N
+
+GELU, QGELU, TANH, GELU_TANH = 1, 2, 3, 4
+
+
+def _rows(ld):
+    return N.rows(ld)
+
+
+def _colsum(x, out):
+    rows = x.numel() // x.shape[-1]
+    N.colsum(x, rows, x.shape[-1], x.shape[-1], out, accumulate=True)
+
+
+def _wgrad(dy, x, gW):
+    """gW[out][in] += dy^T x  (dy [R][out], x [R][in]) — TN GEMM accumulating in fp32."""
+    R = dy.numel() // dy.shape[-1]
+    N.gemm(dy, x, gW, gW.shape[0], gW.shape[1], R, trans=1, lda=dy.shape[-1], ldb=x.shape[-1],
+           accumulate=True)
+
+
+def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=None):
+    """y = act(x W^T + b) (+ resid); W [out][in] compute dtype."""
+    R = x.numel() // x.shape[-1]
+    n_out = W.shape[0]
+    if out is None:
+        out = torch.empty(R, n_out, device=x.device, dtype=out_dtype or x.dtype)
+    N.gemm(x, W, out, R, n_out, x.shape[-1], bias=bias, act=act, aux=aux, resid=resid)
+    return out
+
+
+def _dgrad(dy, WT, resid=None, act=0, dact=None, out=None):
+    """dx = dy W (+ resid), using the transposed shadow WT [in][out]; optionally times act'(dact)."""
+    R = dy.numel() // dy.shape[-1]
+    n_in = WT.shape[0]
+    if out is None:
+        out = torch.empty(R, n_in, device=dy.device, dtype=dy.dtype)
+    N.gemm(dy, WT, out, R, n_in, dy.shape[-1], resid=resid, act=act, dact=dact)
+    return out
+
+
+class LayerRefs:
+    """Names of one layer's parameters inside a ParamStore (resolved once)."""
+
+    def __init__(self, store, **names):
+        self.store = store
+        self.__dict__.update(names)
+
+
+# ================================================================================================
+# BERT layer (post-LN), lxrt/modeling.py:496-507 (BertSelfattLayer + BertIntermediate + BertOutput)
+# ================================================================================================
+class BertLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps):
+        st = L.store
+        H = x.shape[-1]
+        Wqkv = st.packed(L.qkv_w, "w")
+        bqkv = st.packed(L.qkv_b, "f32").view(-1)
+        qkv = _linear(x, Wqkv, bias=bqkv)
+        o = torch.empty_like(x)
+        lse = torch.empty(P, heads, T, device=x.device)
+        N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
+                   H, lse)
+        s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x)
+        h1 = torch.empty_like(x)
+        m1 = torch.empty(s1.shape[0], device=x.device)
+        r1 = torch.empty_like(m1)
+        N.layernorm_fwd(s1.shape[0], H, s1, _rows(H), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, h1,
+                        _rows(H), m1, r1)
+        z = torch.empty(x.shape[0], st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype)
+        gact = _linear(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU, aux=z)
+        s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1)
+        y = torch.empty_like(x)
+        m2 = torch.empty_like(m1)
+        r2 = torch.empty_like(m1)
+        N.layernorm_fwd(s2.shape[0], H, s2, _rows(H), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y,
+                        _rows(H), m2, r2)
+        ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
+        ctx.meta = (L, P, T, heads)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2 = ctx.saved_tensors
+        L, P, T, heads = ctx.meta
+        st = L.store
+        H = x.shape[-1]
+        dy = dy.contiguous()
+        R = x.shape[0]
+        ds2 = torch.empty_like(dy)
+        N.layernorm_bwd(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
+                        None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b))
+        _wgrad(ds2, gact, st.g(L.out_w))
+        _colsum(ds2, st.g(L.out_b))
+        dz = _dgrad(ds2, st.wt(L.out_w), act=GELU, dact=z)
+        _wgrad(dz, h1, st.g(L.i_w))
+        _colsum(dz, st.g(L.i_b))
+        dh1 = _dgrad(dz, st.wt(L.i_w), resid=ds2)
+        del dz
+        ds1 = torch.empty_like(dy)
+        N.layernorm_bwd(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
+                        None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b))
+        _wgrad(ds1, o, st.g(L.o_w))
+        _colsum(ds1, st.g(L.o_b))
+        do = _dgrad(ds1, st.wt(L.o_w))
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(P, heads, T, device=x.device)
+        N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
+                   H, do, H, lse, delta, dqkv, 3 * H)
+        _wgrad(dqkv, x, st.packed(L.qkv_w, "g"))
+        _colsum(dqkv, st.packed(L.qkv_b, "g").view(-1))
+        dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
+        return dx, None, None, None, None, None, None, None
+
+
+# ================================================================================================
+# CLIP ViT residual attention block (pre-LN), clip/model.py:204-226
+# ================================================================================================
+class VitBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, anchor, L, P, T, heads, eps):
+        st = L.store
+        W = h.shape[-1]
+        R = h.shape[0]
+        m1 = torch.empty(R, device=h.device)
+        r1 = torch.empty_like(m1)
+        hn = torch.empty_like(h)
+        N.layernorm_fwd(R, W, h, _rows(W), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, hn, _rows(W),
+                        m1, r1)
+        qkv = _linear(hn, st.w(L.in_w), bias=st.f32(L.in_b))
+        o = torch.empty_like(h)
+        lse = torch.empty(P, heads, T, device=h.device)
+        N.attn_fwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
+                   lse)
+        x1 = _linear(o, st.w(L.out_w), bias=st.f32(L.out_b), resid=h)
+        m2 = torch.empty_like(m1)
+        r2 = torch.empty_like(m1)
+        hn2 = torch.empty_like(h)
+        N.layernorm_fwd(R, W, x1, _rows(W), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, hn2, _rows(W),
+                        m2, r2)
+        z = torch.empty(R, st.w(L.fc_w).shape[0], device=h.device, dtype=h.dtype)
+        gact = _linear(hn2, st.w(L.fc_w), bias=st.f32(L.fc_b), act=QGELU, aux=z)
+        x2 = _linear(gact, st.w(L.proj_w), bias=st.f32(L.proj_b), resid=x1)
+        ctx.save_for_backward(h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact)
+        ctx.meta = (L, P, T, heads)
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact = ctx.saved_tensors
+        L, P, T, heads = ctx.meta
+        st = L.store
+        W = h.shape[-1]
+        R = h.shape[0]
+        dx2 = dx2.contiguous()
+        _wgrad(dx2, gact, st.g(L.proj_w))
+        _colsum(dx2, st.g(L.proj_b))
+        dz = _dgrad(dx2, st.wt(L.proj_w), act=QGELU, dact=z)
+        _wgrad(dz, hn2, st.g(L.fc_w))
+        _colsum(dz, st.g(L.fc_b))
+        dhn2 = _dgrad(dz, st.wt(L.fc_w))
+        del dz
+        dx1 = torch.empty_like(h)
+        N.layernorm_bwd(R, W, dhn2, _rows(W), x1, _rows(W), m2, r2, st.f32(L.ln2_w), dx1, _rows(W),
+                        dx2, _rows(W), st.g(L.ln2_w), st.g(L.ln2_b))
+        _wgrad(dx1, o, st.g(L.out_w))
+        _colsum(dx1, st.g(L.out_b))
+        do = _dgrad(dx1, st.wt(L.out_w))
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(P, heads, T, device=h.device)
+        N.attn_bwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
+                   do, W, lse, delta, dqkv, 3 * W)
+        _wgrad(dqkv, hn, st.g(L.in_w))
+        _colsum(dqkv, st.g(L.in_b))
+        dhn = _dgrad(dqkv, st.wt(L.in_w))
+        dh = torch.empty_like(h)
+        N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
+                        dx1, _rows(W), st.g(L.ln1_w), st.g(L.ln1_b))
+        return dh, None, None, None, None, None, None
+
+
+# ================================================================================================
+# ViT stem: pair-image gather + patchify GEMM + class token + positional quirk + ln_pre
+# ================================================================================================
+class VitStemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, images, pairs, anchor, L, patch, eps, cdtype):
+        st = L.store
+        B, Nst, _, R_, _ = images.shape
+        npair = pairs.shape[1]
+        P = B * npair
+        g = R_ // patch
+        gg = g * g
+        ntok = 1 + 2 * gg
+        Wc = st.w(L.conv_w)  # [W][3][p][p] -> [W][3p^2]
+        W = Wc.shape[0]
+        Wc = Wc.reshape(W, -1)
+        patches = torch.empty(P * 2 * gg, 3 * patch * patch, device=images.device, dtype=cdtype)
+        N.vit_im2col(B, Nst, npair, R_, patch, images, pairs, patches)
+        po = _linear(patches, Wc)
+        del patches
+        x0 = torch.empty(P * ntok, W, device=images.device, dtype=cdtype)
+        h0 = torch.empty_like(x0)
+        mean = torch.empty(P * ntok, device=images.device)
+        rstd = torch.empty_like(mean)
+        N.vit_embed_fwd(P, ntok, W, gg, po, st.f32(L.cls), st.f32(L.pos), st.f32(L.ln_w),
+                        st.f32(L.ln_b), eps, x0, h0, mean, rstd)
+        ctx.save_for_backward(images, pairs, x0, mean, rstd)
+        ctx.meta = (L, patch, cdtype, P, ntok, W, gg)
+        return h0
+
+    @staticmethod
+    def backward(ctx, dh0):
+        images, pairs, x0, mean, rstd = ctx.saved_tensors
+        L, patch, cdtype, P, ntok, W, gg = ctx.meta
+        st = L.store
+        B, Nst, _, R_, _ = images.shape
+        dpo = torch.empty(P * (ntok - 1), W, device=x0.device, dtype=cdtype)
+        N.vit_embed_bwd(P, ntok, W, gg, dh0.contiguous(), x0, mean, rstd, st.f32(L.ln_w), dpo,
+                        st.g(L.cls), st.g(L.pos), st.g(L.ln_w), st.g(L.ln_b))
+        patches = torch.empty(P * 2 * gg, 3 * patch * patch, device=x0.device, dtype=cdtype)
+        N.vit_im2col(B, Nst, pairs.shape[1], R_, patch, images, pairs, patches)  # recompute
+        _wgrad(dpo, patches, st.g(L.conv_w).view(W, -1))
+        return None, None, None, None, None, None, None
+
+
+# ================================================================================================
+# ViT output projection (x @ proj, no ln_post: clip/model.py:301-304, lxrt:783)
+# ================================================================================================
+class VitProjFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, anchor, L):
+        st = L.store
+        out = _linear(h, st.wt(L.proj))  # B(k=w, n=e) = proj[w][e] -> NT operand proj^T [E][W]
+        ctx.save_for_backward(h)
+        ctx.meta = L
+        return out
+
+    @staticmethod
+    def backward(ctx, dv):
+        (h,) = ctx.saved_tensors
+        L = ctx.meta
+        st = L.store
+        dv = dv.contiguous()
+        gp = st.g(L.proj)  # [W][E] += h^T dv
+        R = h.shape[0]
+        N.gemm(h, dv, gp, gp.shape[0], gp.shape[1], R, trans=1, lda=h.shape[-1], ldb=dv.shape[-1],
+               accumulate=True)
+        dh = _dgrad(dv, st.w(L.proj))  # dh[r][w] = sum_e dv[r][e] proj[w][e]
+        return dh, None, None
+
+
+# ================================================================================================
+# Joint input: visn_fc (Linear + LN) and BertEmbeddings (+LN) written in place into the two
+# halves of the joint [P][T][H] buffer; additive key mask (lxrt/modeling.py:1537-1545, 1071-1094)
+# ================================================================================================
+class JointInputFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, vout, ids, tt, attn_mask, anchor, L, P, Lt, Tv, eps, cdtype):
+        st = L.store
+        H = st.f32(L.word).shape[1]
+        T = Lt + Tv
+        dev = ids.device
+        joint = torch.empty(P * T, H, device=dev, dtype=cdtype)
+        me = torch.empty(P * Lt, device=dev)
+        re = torch.empty_like(me)
+        N.embed_ln_fwd(P, Lt, H, ids, tt, st.f32(L.word), st.f32(L.pos), st.f32(L.type),
+                       st.f32(L.eln_w), st.f32(L.eln_b), eps, joint, T * H, me, re)
+        saved = [ids, tt, me, re]
+        if vout is not None:
+            vpre = _linear(vout, st.w(L.v_w), bias=st.f32(L.v_b))
+            mv = torch.empty(P * Tv, device=dev)
+            rv = torch.empty_like(mv)
+            N.layernorm_fwd(P * Tv, H, vpre, _rows(H), st.f32(L.vln_w), st.f32(L.vln_b), eps,
+                            joint[Lt:], N.rows(H, T * H, Tv), mv, rv)
+            saved += [vout, vpre, mv, rv]
+        key_bias = torch.zeros(P, T, device=dev)
+        key_bias[:, :Lt] = (1.0 - attn_mask.float()) * -10000.0
+        ctx.save_for_backward(*saved)
+        ctx.meta = (L, P, Lt, Tv, vout is not None)
+        ctx.mark_non_differentiable(key_bias)
+        return joint, key_bias
+
+    @staticmethod
+    def backward(ctx, djoint, _dkb):
+        L, P, Lt, Tv, has_v = ctx.meta
+        st = L.store
+        sv = ctx.saved_tensors
+        ids, tt, me, re = sv[:4]
+        H = st.f32(L.word).shape[1]
+        T = Lt + Tv
+        djoint = djoint.contiguous()
+        N.embed_ln_bwd(P, Lt, H, ids, tt, st.f32(L.word), st.f32(L.pos), st.f32(L.type),
+                       st.f32(L.eln_w), me, re, djoint, T * H, st.g(L.word), st.g(L.pos),
+                       st.g(L.type), st.g(L.eln_w), st.g(L.eln_b))
+        dvout = None
+        if has_v:
+            vout, vpre, mv, rv = sv[4:]
+            dvpre = torch.empty_like(vpre)
+            N.layernorm_bwd(P * Tv, H, djoint[Lt:], N.rows(H, T * H, Tv), vpre, _rows(H), mv, rv,
+                            st.f32(L.vln_w), dvpre, _rows(H), None, _rows(H), st.g(L.vln_w),
+                            st.g(L.vln_b))
+            _wgrad(dvpre, vout, st.g(L.v_w))
+            _colsum(dvpre, st.g(L.v_b))
+            dvout = _dgrad(dvpre, st.wt(L.v_w))
+        return dvout, None, None, None, None, None, None, None, None, None, None
+
+
+# ================================================================================================
+# generic pieces used by the (small, fp32) BERSON head
+# ================================================================================================
+class LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b); W, b taken from a ParamStore (grads accumulated into its buffer)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, store, wname, bname, act):
+        x = x.contiguous()
+        shp = x.shape
+        x2 = x.view(-1, shp[-1])
+        W = store.w(wname)
+        aux = None
+        if act:
+            aux = torch.empty(x2.shape[0], W.shape[0], device=x.device, dtype=x.dtype)
+        y = _linear(x2, W, bias=store.f32(bname) if bname else None, act=act, aux=aux)
+        ctx.save_for_backward(x2, aux if act else None)
+        ctx.meta = (store, wname, bname, act, shp)
+        return y.view(*shp[:-1], W.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, aux = ctx.saved_tensors
+        store, wname, bname, act, shp = ctx.meta
+        dy = dy.contiguous().view(-1, dy.shape[-1])
+        if act:
+            dz = torch.empty_like(dy)
+            N.act_bwd(aux, dy, dz, act)
+            dy = dz
+        _wgrad(dy, x2, store.g(wname))
+        if bname:
+            _colsum(dy, store.g(bname))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dy, store.wt(wname)).view(shp)
+        return dx, None, None, None, None, None
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, store, prefix, eps):
+        x = x.contiguous()
+        shp = x.shape
+        C = shp[-1]
+        R = x.numel() // C
+        y = torch.empty_like(x)
+        m = torch.empty(R, device=x.device)
+        r = torch.empty_like(m)
+        N.layernorm_fwd(R, C, x, _rows(C), store.f32(prefix + ".weight"), store.f32(prefix + ".bias"),
+                        eps, y, _rows(C), m, r)
+        ctx.save_for_backward(x, m, r)
+        ctx.meta = (store, prefix)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, m, r = ctx.saved_tensors
+        store, prefix = ctx.meta
+        C = x.shape[-1]
+        R = x.numel() // C
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        N.layernorm_bwd(R, C, dy, _rows(C), x, _rows(C), m, r, store.f32(prefix + ".weight"), dx,
+                        _rows(C), None, _rows(C), store.g(prefix + ".weight"),
+                        store.g(prefix + ".bias"))
+        return dx, None, None, None, None
+
+
+class SmallAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, key_bias, heads):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, T, D = q.shape
+        d = D // heads
+        out = torch.empty_like(q)
+        probs = torch.empty(B, heads, T, T, device=q.device)
+        N.small_attn_fwd(B, T, heads, d, q, k, v, key_bias, 1.0 / math.sqrt(d), out, probs)
+        ctx.save_for_backward(q, k, v, probs)
+        ctx.heads = heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, probs = ctx.saved_tensors
+        B, T, D = q.shape
+        d = D // ctx.heads
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        N.small_attn_bwd(B, T, ctx.heads, d, q, k, v, probs, dout.contiguous(), 1.0 / math.sqrt(d),
+                         dq, dk, dv)
+        return dq, dk, dv, None, None
+
+
+class SpanPoolFn(torch.autograd.Function):
+    """HierarchicalAttention span pooling over the text rows of the joint output."""
+
+    @staticmethod
+    def forward(ctx, top, score, sep):
+        P, Lt, H = top.shape
+        top = top.contiguous()
+        probs = torch.empty(P, 2, Lt, device=top.device)
+        mix = torch.empty(P, 2, H, device=top.device)
+        N.span_pool_fwd(P, Lt, H, top, Lt * H, score.contiguous(), sep, probs, mix)
+        ctx.save_for_backward(top, probs, sep)
+        return mix
+
+    @staticmethod
+    def backward(ctx, dmix):
+        top, probs, sep = ctx.saved_tensors
+        P, Lt, H = top.shape
+        dscore = torch.empty(P, Lt, device=top.device)
+        dtop = torch.zeros_like(top)
+        N.span_pool_bwd(P, Lt, H, top, Lt * H, probs, sep, dmix.contiguous(), dscore, dtop)
+        return dtop, dscore, None
+
+
+class PointerFn(torch.autograd.Function):
+    """e = tanh_linear(tanh(q + key + okey)) -> masked log-softmax -> per-step NLL."""
+
+    @staticmethod
+    def forward(ctx, q, key, okey, anchor, store, wname, bname, pointed, tgt_len, target):
+        B, Nn, H = q.shape
+        q, key, okey = q.contiguous(), key.contiguous(), okey.contiguous()
+        logp = torch.empty(B, Nn, Nn, device=q.device)
+        nll = torch.empty(B, Nn, device=q.device)
+        N.pointer_fwd(B, Nn, H, q, key, okey, store.f32(wname).view(-1), store.f32(bname), pointed,
+                      tgt_len, target, logp, nll)
+        ctx.save_for_backward(q, key, okey, logp, pointed, tgt_len, target)
+        ctx.meta = (store, wname, bname)
+        ctx.mark_non_differentiable(logp)
+        return nll, logp
+
+    @staticmethod
+    def backward(ctx, dnll, _dlogp):
+        q, key, okey, logp, pointed, tgt_len, target = ctx.saved_tensors
+        store, wname, bname = ctx.meta
+        B, Nn, H = q.shape
+        dq, dkey = torch.empty_like(q), torch.empty_like(key)
+        dokey = torch.zeros_like(okey)
+        N.pointer_bwd(B, Nn, H, q, key, okey, store.f32(wname).view(-1), logp, pointed, tgt_len,
+                      target, dnll.contiguous(), dq, dkey, dokey, store.g(wname).view(-1),
+                      store.g(bname))
+        return dq, dkey, dokey, None, None, None, None, None, None, None

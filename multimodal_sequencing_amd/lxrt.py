@@ -1,0 +1,234 @@
+"""LXRTModel in VisualBERT style with a CLIP ViT visual backbone — the inner encoder of the path.
+
+Mirrors the reference's drop-in surface:
+  * models/CLIP/src/lxrt/modeling.py  LXRTModel (:1456-1598), LXRTEncoder (:737-1122),
+    BertEmbeddings (:342-370), BertLayer (:496-507), VisualFeatEncoder (:569-602), BertPooler
+  * models/CLIP/clip/model.py         VisualTransformer (:242-305) with img_len = 2 (BERSON input)
+  * same constructor kwargs, same forward signature and return structure
+    `((lang_feats, visn_feats), pooled)`, same state-dict key names.
+
+Compute runs through the mmseq HIP kernels (kernels.py); there is no CPU path. Parameters live in
+one flat ParamStore (params.py); the module tree only carries named views of it.
+"""
+import math
+from types import SimpleNamespace
+
+import torch
+from torch import nn
+
+from . import kernels as K
+from .params import ParamStore, Spec, attach_tree, linear_specs, ln_specs, normal, ones, zeros
+
+VIT = "encoder.visual_model.visual."
+
+# CLIP vision configs (clip/clip.py:18-23 + the two ViT sizes the BASELINE configs name)
+CLIP_VISION = {
+    "ViT-B/32": dict(width=768, layers=12, patch=32, res=224, embed=512),
+    "ViT-B/16": dict(width=768, layers=12, patch=16, res=224, embed=512),
+    "ViT-L/14": dict(width=1024, layers=24, patch=14, res=224, embed=768),
+}
+
+
+class LXRTConfig(SimpleNamespace):
+    """Subset of lxrt BertConfig (:147-336) that the path reads."""
+
+    def __init__(self, vocab_size=50265, hidden_size=768, num_hidden_layers=12,
+                 num_attention_heads=12, intermediate_size=3072, max_position_embeddings=514,
+                 type_vocab_size=1, hidden_act="gelu", initializer_range=0.02, **kw):
+        super().__init__(vocab_size=vocab_size, hidden_size=hidden_size,
+                         num_hidden_layers=num_hidden_layers,
+                         num_attention_heads=num_attention_heads,
+                         intermediate_size=intermediate_size,
+                         max_position_embeddings=max_position_embeddings,
+                         type_vocab_size=type_vocab_size, hidden_act=hidden_act,
+                         initializer_range=initializer_range, **kw)
+
+
+def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25):
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    std = cfg.initializer_range
+    sp = [Spec("embeddings.word_embeddings.weight", (cfg.vocab_size, H), normal(std)),
+          Spec("embeddings.position_embeddings.weight", (cfg.max_position_embeddings, H),
+               normal(std)),
+          Spec("embeddings.token_type_embeddings.weight", (cfg.type_vocab_size, H),
+               normal(std))]
+    sp += ln_specs("embeddings.LayerNorm", H)
+    if not text_part:
+        E = vision["embed"]
+        sp += linear_specs("encoder.visn_fc.visn_fc", E, H, std=std)
+        sp += ln_specs("encoder.visn_fc.visn_layer_norm", H)
+        sp += linear_specs("encoder.visn_fc.box_fc", 4, H, std=std, transpose=False)
+        sp += ln_specs("encoder.visn_fc.box_layer_norm", H)
+    for i in range(cfg.num_hidden_layers):
+        b = f"encoder.layer.{i}."
+        a = b + "attention.self."
+        sp += [Spec(a + "query.weight", (H, H), normal(std), transpose=True, pack=f"qkvw{i}"),
+               Spec(a + "key.weight", (H, H), normal(std), transpose=True, pack=f"qkvw{i}"),
+               Spec(a + "value.weight", (H, H), normal(std), transpose=True, pack=f"qkvw{i}"),
+               Spec(a + "query.bias", (H,), zeros, pack=f"qkvb{i}"),
+               Spec(a + "key.bias", (H,), zeros, pack=f"qkvb{i}"),
+               Spec(a + "value.bias", (H,), zeros, pack=f"qkvb{i}")]
+        sp += linear_specs(b + "attention.output.dense", H, H, std=std)
+        sp += ln_specs(b + "attention.output.LayerNorm", H)
+        sp += linear_specs(b + "intermediate.dense", H, I, std=std)
+        sp += linear_specs(b + "output.dense", I, H, std=std)
+        sp += ln_specs(b + "output.LayerNorm", H)
+    if not text_part:
+        W, L, p, R, E = (vision[k] for k in ("width", "layers", "patch", "res", "embed"))
+        scale = W ** -0.5
+        g = R // p
+        sp += [Spec(VIT + "class_embedding", (W,), normal(scale)),
+               Spec(VIT + "positional_embedding", (g * g + 1, W), normal(scale)),
+               Spec(VIT + "proj", (W, E), normal(scale), transpose=True),
+               Spec(VIT + "conv1.weight", (W, 3, p, p), normal(std))]
+        sp += ln_specs(VIT + "ln_pre", W)
+        for i in range(L):
+            b = f"{VIT}transformer.resblocks.{i}."
+            sp += [Spec(b + "attn.in_proj_weight", (3 * W, W), normal(std), transpose=True),
+                   Spec(b + "attn.in_proj_bias", (3 * W,), zeros)]
+            sp += linear_specs(b + "attn.out_proj", W, W, std=std)
+            sp += ln_specs(b + "ln_1", W)
+            sp += linear_specs(b + "mlp.c_fc", W, 4 * W, std=std)
+            sp += linear_specs(b + "mlp.c_proj", 4 * W, W, std=std)
+            sp += ln_specs(b + "ln_2", W)
+        sp += ln_specs(VIT + "ln_post", W)
+        # RN50-only modules, constructed by the reference regardless (VISUAL_CONFIG flags,
+        # lxrt:819-822); unused on the ViT path but part of the state dict
+        sp += [Spec("encoder.visual_pos.x_position_embedding.weight", (pos_num, E), normal(std)),
+               Spec("encoder.visual_pos.y_position_embedding.weight", (pos_num, E), normal(std)),
+               Spec("encoder.visual_token_type.token_type_embedding.weight",
+                    (5, E), normal(std))]  # hard-coded max_story_length = 5 (lxrt:666-667)
+    sp += linear_specs("pooler.dense", H, H, std=std, transpose=False)
+    return sp
+
+
+class LXRTModel(nn.Module):
+    """VisualBERT-style LXRT encoder over cat(text tokens, CLIP-ViT patch tokens)."""
+
+    def __init__(self, config, multimodal_text_part=False, multimodal_img_part=False, cls_id=0,
+                 sep_id=2, max_story_length=5, hl_include_objectives=None, mlm_ignore_index=-100,
+                 clip_model_name="ViT-B/16", num_labels=None, device="cuda",
+                 compute_dtype=torch.bfloat16, vision=None, **kw):
+        super().__init__()
+        if multimodal_img_part:
+            raise NotImplementedError("image-only pretraining (config 2) is a 'next' row (SURVEY §8f)")
+        if num_labels is not None:
+            raise NotImplementedError("topological-sort head is out of scope (SURVEY §2 row 3)")
+        self.config = config
+        self.text_part = multimodal_text_part
+        self.cls_id, self.sep_id = cls_id, sep_id
+        self.clip_model_name = clip_model_name
+        self.vision = dict(vision or CLIP_VISION[clip_model_name])
+        self.img_len = 2  # VISUAL_CONFIG.max_subsample_image_length for BERSON input (lxrt:770)
+        specs = _lxrt_specs(config, self.vision, multimodal_text_part, max_story_length)
+        self.store = ParamStore(specs, device, compute_dtype)
+        self.store.init_weights(seed=kw.get("seed", 0))
+        attach_tree(self, self.store.params)
+        self._anchor = torch.zeros((), device=device, requires_grad=True)
+        self._build_refs()
+
+    # -- parameter groups per layer ---------------------------------------------------------
+    def _build_refs(self):
+        st = self.store
+        self.layer_refs = []
+        for i in range(self.config.num_hidden_layers):
+            b = f"encoder.layer.{i}."
+            a = b + "attention.self."
+            self.layer_refs.append(K.LayerRefs(
+                st, qkv_w=[a + "query.weight", a + "key.weight", a + "value.weight"],
+                qkv_b=[a + "query.bias", a + "key.bias", a + "value.bias"],
+                o_w=b + "attention.output.dense.weight", o_b=b + "attention.output.dense.bias",
+                ln1_w=b + "attention.output.LayerNorm.weight",
+                ln1_b=b + "attention.output.LayerNorm.bias",
+                i_w=b + "intermediate.dense.weight", i_b=b + "intermediate.dense.bias",
+                out_w=b + "output.dense.weight", out_b=b + "output.dense.bias",
+                ln2_w=b + "output.LayerNorm.weight", ln2_b=b + "output.LayerNorm.bias"))
+        e = "embeddings."
+        v = "encoder.visn_fc."
+        self.input_refs = K.LayerRefs(
+            st, word=e + "word_embeddings.weight", pos=e + "position_embeddings.weight",
+            type=e + "token_type_embeddings.weight", eln_w=e + "LayerNorm.weight",
+            eln_b=e + "LayerNorm.bias", v_w=v + "visn_fc.weight", v_b=v + "visn_fc.bias",
+            vln_w=v + "visn_layer_norm.weight", vln_b=v + "visn_layer_norm.bias")
+        if not self.text_part:
+            self.stem_refs = K.LayerRefs(st, conv_w=VIT + "conv1.weight", cls=VIT + "class_embedding",
+                                         pos=VIT + "positional_embedding", ln_w=VIT + "ln_pre.weight",
+                                         ln_b=VIT + "ln_pre.bias")
+            self.proj_refs = K.LayerRefs(st, proj=VIT + "proj")
+            self.block_refs = []
+            for i in range(self.vision["layers"]):
+                b = f"{VIT}transformer.resblocks.{i}."
+                self.block_refs.append(K.LayerRefs(
+                    st, in_w=b + "attn.in_proj_weight", in_b=b + "attn.in_proj_bias",
+                    out_w=b + "attn.out_proj.weight", out_b=b + "attn.out_proj.bias",
+                    ln1_w=b + "ln_1.weight", ln1_b=b + "ln_1.bias", fc_w=b + "mlp.c_fc.weight",
+                    fc_b=b + "mlp.c_fc.bias", proj_w=b + "mlp.c_proj.weight",
+                    proj_b=b + "mlp.c_proj.bias", ln2_w=b + "ln_2.weight", ln2_b=b + "ln_2.bias"))
+
+    @property
+    def compute_dtype(self):
+        return self.store.compute_dtype
+
+    def set_compute_dtype(self, dtype):
+        self.store.set_compute_dtype(dtype)
+
+    # -- forward ----------------------------------------------------------------------------
+    def visual_forward(self, images, pairs_list):
+        """CLIP ViT over the paired images of every ordered pair (img_len = 2):
+        images [B][N][3][R][R] f32 (device), pairs_list [B][npair][2] -> [P*Tv][E]."""
+        st = self.store
+        V = self.vision
+        W, patch = V["width"], V["patch"]
+        heads = W // 64
+        B, npair = pairs_list.shape[:2]
+        P = B * npair
+        g = images.shape[-1] // patch
+        Tv = 1 + 2 * g * g
+        cd = st.compute_dtype
+        h = K.VitStemFn.apply(images, pairs_list, self._anchor, self.stem_refs, patch, 1e-5, cd)
+        for L in self.block_refs:
+            h = K.VitBlockFn.apply(h, self._anchor, L, P, Tv, heads, 1e-5)
+        return K.VitProjFn.apply(h, self._anchor, self.proj_refs), Tv
+
+    def encode_joint(self, input_ids, attention_mask, token_type_ids=None, images=None,
+                     pairs_list=None):
+        """Run embeddings (+ ViT + visn_fc) and the joint BERT stack.
+        Returns the joint activation [P][T][H] (compute dtype) and Lt."""
+        st = self.store
+        if st.shadow_stale:
+            st.refresh_shadows()
+        P, Lt = input_ids.shape
+        if token_type_ids is None:
+            token_type_ids = torch.zeros_like(input_ids)
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        vout, Tv = None, 0
+        if not self.text_part and images is not None:
+            vout, Tv = self.visual_forward(images, pairs_list)
+        T = Lt + Tv
+        x, key_bias = K.JointInputFn.apply(vout, input_ids.contiguous(), token_type_ids.contiguous(),
+                                           attention_mask, self._anchor, self.input_refs, P, Lt,
+                                           Tv, 1e-12, st.compute_dtype)
+        heads = self.config.num_attention_heads
+        for L in self.layer_refs:
+            x = K.BertLayerFn.apply(x, key_bias, self._anchor, L, P, T, heads, 1e-12)
+        return x.view(P, T, -1), Lt
+
+    def forward(self, input_ids, token_type_ids=None, attention_mask=None, visual_feats=None,
+                visual_attention_mask=None, pretraining_objective=None, labels=None,
+                pairs_list=None):
+        """LXRTModel.forward (:1513-1598). `visual_feats` is either the reference's
+        [2P][3][R][R] pair-image tensor, or (images [B][N][3][R][R], pairs_list) via the
+        `pairs_list` kwarg so the pair gather happens on device."""
+        if visual_feats is not None and pairs_list is None:
+            # reference layout: consecutive image pairs -> treat as B = P stories of 2 images
+            R = visual_feats.shape[-1]
+            imgs = visual_feats.reshape(-1, 2, 3, R, R).float().contiguous()
+            pl = torch.tensor([[[0, 1]]], device=imgs.device).expand(imgs.shape[0], 1, 2).contiguous()
+            visual_feats, pairs_list = imgs, pl
+        joint, Lt = self.encode_joint(input_ids, attention_mask, token_type_ids, visual_feats,
+                                      pairs_list)
+        lang = joint[:, :Lt]
+        visn = joint[:, Lt:] if joint.shape[1] > Lt else None
+        # the pooler is computed but unused on the BERSON path (:1586); expose lang[:,0] as pooled
+        return (lang, visn), lang[:, 0]

@@ -1,0 +1,367 @@
+"""Per-kernel numerics: each HIP kernel (through the C ABI) against a plain fp32 PyTorch reference.
+
+fp32 kernels (exact-fp32 MFMA) are held to ~1e-5 relative; bf16 kernels to bf16 rounding of
+inputs/outputs (~1e-2 relative).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from multimodal_sequencing_amd import _native as nat
+
+DEV = "cuda"
+TOL = {torch.float32: (2e-5, 2e-5), torch.bfloat16: (2e-2, 2e-2)}
+
+
+def _close(a, b, dtype, scale=1.0):
+    rt, at = TOL[dtype]
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= at * scale + rt * scale * ref, f"max err {err} vs ref max {ref}"
+
+
+def _q(x, dtype):
+    return x.to(dtype).float()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 200, 136), (77, 96, 520), (1, 2, 768),
+                                   (513, 768, 768)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3, 4])
+def test_gemm_nt_epilogues(dtype, M, N, K, act):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + act)
+    A = torch.randn(M, K, generator=g).to(DEV, dtype)
+    Bm = torch.randn(N, K, generator=g).to(DEV, dtype) * 0.1
+    bias = torch.randn(N, generator=g).to(DEV)
+    resid = torch.randn(M, N, generator=g).to(DEV, dtype)
+    C = torch.empty(M, N, device=DEV, dtype=dtype)
+    aux = torch.empty(M, N, device=DEV, dtype=dtype) if act else None
+    nat.gemm(A, Bm, C, M, N, K, bias=bias, act=act, aux=aux, resid=resid)
+    z = A.float() @ Bm.float().t() + bias
+    acts = {0: lambda x: x, 1: lambda x: torch.nn.functional.gelu(x), 2: lambda x: x * torch.sigmoid(1.702 * x),
+            3: torch.tanh, 4: lambda x: torch.nn.functional.gelu(x, approximate="tanh")}
+    ref = acts[act](z) + resid.float()
+    _close(C, ref, dtype, scale=max(1.0, math.sqrt(K) / 8))
+    if act:
+        _close(aux, z, dtype, scale=max(1.0, math.sqrt(K) / 8))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 96, 300), (768, 768, 1026), (2, 520, 77)])
+def test_gemm_tn_accumulate(dtype, M, N, K):
+    # dW[M][N] += sum_k dY[k][M] X[k][N]  (wgrad layout)
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    dY = torch.randn(K, M, generator=g).to(DEV, dtype)
+    X = torch.randn(K, N, generator=g).to(DEV, dtype)
+    C0 = torch.randn(M, N, generator=g).to(DEV)
+    C = C0.clone()
+    nat.gemm(dY, X, C, M, N, K, trans=1, accumulate=True)
+    ref = C0 + dY.float().t() @ X.float()
+    _close(C, ref, dtype, scale=max(1.0, math.sqrt(K) / 8))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_dact_and_batched(dtype):
+    g = torch.Generator(device="cpu").manual_seed(3)
+    M, Nn, K, Bt = 96, 64, 128, 3
+    A = torch.randn(Bt, M, K, generator=g).to(DEV, dtype)
+    Bm = torch.randn(Nn, K, generator=g).to(DEV, dtype) * 0.1
+    z = torch.randn(Bt, M, Nn, generator=g).to(DEV, dtype)
+    C = torch.empty(Bt, M, Nn, device=DEV, dtype=dtype)
+    nat.gemm(A, Bm, C, M, Nn, K, batch=Bt, sA=M * K, sB=0, sC=M * Nn, act=1, dact=z)
+    zz = z.float().requires_grad_(True)
+    gz = torch.autograd.grad(torch.nn.functional.gelu(zz).sum(), zz)[0]
+    ref = (A.float() @ Bm.float().t()) * gz
+    _close(C, ref, dtype, scale=2.0)
+
+
+def _attn_ref(qkv, P, T, heads, bias, scale):
+    H = heads * 64
+    q, k, v = qkv.float().view(P, T, 3, heads, 64).unbind(2)
+    s = torch.einsum("pqhd,pkhd->phqk", q, k) * scale
+    if bias is not None:
+        s = s + bias[:, None, None, :]
+    a = torch.softmax(s, -1)
+    return torch.einsum("phqk,pkhd->pqhd", a, v).reshape(P * T, H)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("P,T,heads,masked", [(2, 64, 1, False), (3, 129, 2, True), (2, 33, 2, True),
+                                              (1, 513, 12, True), (2, 393, 2, False)])
+def test_attention_fwd_bwd(dtype, P, T, heads, masked):
+    g = torch.Generator(device="cpu").manual_seed(P * T + heads)
+    H = heads * 64
+    qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, dtype)
+    bias = None
+    if masked:
+        m = (torch.rand(P, T, generator=g) > 0.3).float()
+        m[:, 0] = 1
+        bias = ((1 - m) * -10000.0).to(DEV)
+    scale = 1 / 8
+    out = torch.empty(P * T, H, device=DEV, dtype=dtype)
+    lse = torch.empty(P, heads, T, device=DEV)
+    nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse)
+    qf = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qf, P, T, heads, bias, scale)
+    _close(out, ref, dtype)
+    dout = torch.randn(P * T, H, generator=g).to(DEV, dtype)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(P, heads, T, device=DEV)
+    nat.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, dout, H, lse, delta,
+               dqkv, 3 * H)
+    (ref_g,) = torch.autograd.grad(ref, qf, dout.float())
+    _close(dqkv, ref_g, dtype, scale=2.0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols,eps", [(100, 768, 1e-12), (7, 128, 1e-5), (300, 96, 1e-6)])
+def test_layernorm(dtype, rows, cols, eps):
+    g = torch.Generator(device="cpu").manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, generator=g) * 2 + 0.5).to(DEV, dtype)
+    gamma = (1 + 0.1 * torch.randn(cols, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(cols, generator=g)).to(DEV)
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    nat.layernorm_fwd(rows, cols, x, nat.rows(cols), gamma, beta, eps, y, nat.rows(cols), mean, rstd)
+    xf = x.float().requires_grad_(True)
+    gf = gamma.clone().requires_grad_(True)
+    bf = beta.clone().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xf, (cols,), gf, bf, eps)
+    _close(y, ref, dtype)
+    dy = torch.randn(rows, cols, generator=g).to(DEV, dtype)
+    dres = torch.randn(rows, cols, generator=g).to(DEV, dtype)
+    dx = torch.empty_like(x)
+    dg = torch.ones(cols, device=DEV)
+    db = torch.ones(cols, device=DEV)
+    nat.layernorm_bwd(rows, cols, dy, nat.rows(cols), x, nat.rows(cols), mean, rstd, gamma, dx,
+                    nat.rows(cols), dres, nat.rows(cols), dg, db)
+    rdx, rdg, rdb = torch.autograd.grad(ref, (xf, gf, bf), dy.float())
+    _close(dx, rdx + dres.float(), dtype, scale=2.0)
+    _close(dg, rdg + 1, torch.float32, scale=10.0 if dtype == torch.float32 else 500.0)
+    _close(db, rdb + 1, torch.float32, scale=10.0 if dtype == torch.float32 else 500.0)
+
+
+def test_layernorm_strided_rows():
+    # write the visual half of a [P][T][H] joint buffer in place (two-level strides)
+    P, Lt, Tv, H = 3, 5, 7, 64
+    x = torch.randn(P * Tv, H, device=DEV)
+    joint = torch.zeros(P, Lt + Tv, H, device=DEV)
+    g1 = torch.ones(H, device=DEV)
+    b0 = torch.zeros(H, device=DEV)
+    mean = torch.empty(P * Tv, device=DEV)
+    rstd = torch.empty(P * Tv, device=DEV)
+    nat.layernorm_fwd(P * Tv, H, x, nat.rows(H), g1, b0, 1e-12, joint[:, Lt:], nat.rows(H, (Lt + Tv) * H, Tv),
+                    mean, rstd)
+    ref = torch.nn.functional.layer_norm(x, (H,), eps=1e-12).view(P, Tv, H)
+    torch.testing.assert_close(joint[:, Lt:], ref, rtol=1e-5, atol=1e-5)
+    assert joint[:, :Lt].abs().max().item() == 0
+
+
+def test_small_attention():
+    B, T, heads, d = 3, 5, 8, 16
+    g = torch.Generator(device="cpu").manual_seed(0)
+    q, k, v = (torch.randn(B, T, heads * d, generator=g).to(DEV) for _ in range(3))
+    m = torch.ones(B, T)
+    m[1, 3:] = 0
+    bias = ((1 - m) * -10000.0).to(DEV)
+    out = torch.empty_like(q)
+    probs = torch.empty(B, heads, T, T, device=DEV)
+    nat.small_attn_fwd(B, T, heads, d, q, k, v, bias, d ** -0.5, out, probs)
+    qf, kf, vf = (t.clone().requires_grad_(True) for t in (q, k, v))
+    s = torch.einsum("bqhd,bkhd->bhqk", qf.view(B, T, heads, d), kf.view(B, T, heads, d)) * d ** -0.5
+    a = torch.softmax(s + bias[:, None, None, :], -1)
+    ref = torch.einsum("bhqk,bkhd->bqhd", a, vf.view(B, T, heads, d)).reshape(B, T, heads * d)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    do = torch.randn_like(q)
+    dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+    nat.small_attn_bwd(B, T, heads, d, q, k, v, probs, do, d ** -0.5, dq, dk, dv)
+    rq, rk, rv = torch.autograd.grad(ref, (qf, kf, vf), do)
+    for a_, b_ in ((dq, rq), (dk, rk), (dv, rv)):
+        torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_span_pool(dtype):
+    P, Lt, H = 6, 17, 96
+    g = torch.Generator(device="cpu").manual_seed(1)
+    top = torch.randn(P, Lt + 4, H, generator=g).to(DEV, dtype)  # ld_pair > Lt*H (joint rows)
+    score = torch.randn(P, Lt, generator=g).to(DEV)
+    sep = torch.tensor([[3, 9], [7, 16], [1, 2], [5, 12], [8, 16], [2, 16]], device=DEV)
+    probs = torch.empty(P, 2, Lt, device=DEV)
+    mix = torch.empty(P, 2, H, device=DEV)
+    nat.span_pool_fwd(P, Lt, H, top, (Lt + 4) * H, score, sep, probs, mix)
+    tf = top[:, :Lt].float().clone().requires_grad_(True)
+    sf = score.clone().requires_grad_(True)
+    pos = torch.arange(Lt, device=DEV)[None]
+    m0 = ((pos >= 1) & (pos <= sep[:, :1])).float()
+    m1 = ((pos > sep[:, :1]) & (pos <= sep[:, 1:])).float()
+    sel = torch.stack([m0, m1], 1)
+    a = torch.softmax(sel * sf[:, None] + (1 - sel) * -10000.0, -1)
+    ref = a @ tf
+    _close(mix, ref, dtype)
+    dmix = torch.randn(P, 2, H, generator=g).to(DEV)
+    dscore = torch.empty(P, Lt, device=DEV)
+    dtop = torch.zeros_like(top)
+    nat.span_pool_bwd(P, Lt, H, top, (Lt + 4) * H, probs, sep, dmix, dscore, dtop)
+    rt, rs = torch.autograd.grad(ref, (tf, sf), dmix)
+    _close(dtop[:, :Lt], rt, dtype)
+    _close(dscore, rs, torch.float32, scale=5.0 if dtype == torch.float32 else 500.0)
+
+
+def test_pointer_fwd_bwd():
+    B, Nn, H = 3, 5, 64
+    g = torch.Generator(device="cpu").manual_seed(2)
+    q = torch.randn(B, Nn, H, generator=g).to(DEV)
+    key = torch.randn(B, Nn, Nn, H, generator=g).to(DEV)
+    okey = torch.randn(B, Nn, H, generator=g).to(DEV)
+    w = torch.randn(H, generator=g).to(DEV) * 0.2
+    wb = torch.tensor([0.3], device=DEV)
+    target = torch.stack([torch.randperm(Nn, generator=g) for _ in range(B)]).to(DEV)
+    tgt_len = torch.tensor([5, 4, 5], device=DEV)
+    pointed = torch.zeros(B, Nn, Nn, dtype=torch.uint8)
+    for b in range(B):
+        for t in range(1, Nn):
+            pointed[b, t] = pointed[b, t - 1]
+            pointed[b, t, target[b, t - 1]] = 1
+    pointed = pointed.to(DEV)
+    logp = torch.empty(B, Nn, Nn, device=DEV)
+    nll = torch.empty(B, Nn, device=DEV)
+    nat.pointer_fwd(B, Nn, H, q, key, okey, w, wb, pointed, tgt_len, target, logp, nll)
+    qf, kf, of, wf = (t.clone().requires_grad_(True) for t in (q, key, okey, w))
+    e = torch.tanh(qf[:, :, None] + kf + of[:, None]) @ wf + wb
+    valid = torch.arange(Nn, device=DEV)[None] < tgt_len[:, None]
+    e = e.masked_fill(pointed == 1, -1e9).masked_fill(~valid[:, None, :], -1e9)
+    lp = torch.log_softmax(e, -1)
+    rn = -lp.gather(-1, target[:, :, None]).squeeze(-1) * valid
+    torch.testing.assert_close(logp, lp, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(nll, rn, rtol=1e-5, atol=1e-5)
+    dn = torch.randn(B, Nn, generator=g).to(DEV)
+    dq, dkey = torch.empty_like(q), torch.empty_like(key)
+    dok, dw, dwb = torch.zeros_like(okey), torch.zeros_like(w), torch.zeros(1, device=DEV)
+    nat.pointer_bwd(B, Nn, H, q, key, okey, w, logp, pointed, tgt_len, target, dn, dq, dkey, dok, dw,
+                    dwb)
+    rq, rk, ro, rw = torch.autograd.grad(rn, (qf, kf, of, wf), dn)
+    for a_, b_ in ((dq, rq), (dkey, rk), (dok, ro), (dw, rw)):
+        torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-5)
+
+
+def test_adamw_matches_torch():
+    n = 10000
+    g = torch.Generator(device="cpu").manual_seed(4)
+    p = torch.randn(n, generator=g).to(DEV)
+    grad = torch.randn(n, generator=g).to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    ss = torch.empty(1, device=DEV)
+    nat.sumsq(grad, ss)
+    torch.testing.assert_close(ss[0], (grad ** 2).sum(), rtol=1e-5, atol=1e-3)
+    # transformers-3.4 AdamW (trainers/train.py:185): eps added to sqrt(v) BEFORE bias correction,
+    # step = lr * sqrt(1 - b2^t) / (1 - b1^t); decoupled decay p -= lr * wd * p after the update
+    pr, mr, vr = p.double().clone(), torch.zeros(n, dtype=torch.float64, device=DEV), \
+        torch.zeros(n, dtype=torch.float64, device=DEV)
+    shadow = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    lr, wd = 1e-3, 0.01
+    for step in range(1, 4):
+        nat.adamw(p, grad, m, v, None, lr, 0.9, 0.999, 1e-8, wd, step, 1.0, ss, shadow)
+        gr = grad.double() * min(1.0, 1.0 / (ss[0].double().sqrt().item() + 1e-6))
+        mr = 0.9 * mr + 0.1 * gr
+        vr = 0.999 * vr + 0.001 * gr * gr
+        st = lr * math.sqrt(1 - 0.999 ** step) / (1 - 0.9 ** step)
+        pr = pr - st * mr / (vr.sqrt() + 1e-8)
+        pr = pr - lr * wd * pr
+    torch.testing.assert_close(p, pr.float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(shadow.float(), p.bfloat16().float())
+
+
+def test_colsum_and_cast():
+    x = torch.randn(1000, 300, device=DEV).bfloat16()
+    out = torch.ones(300, device=DEV)
+    nat.colsum(x, 1000, 300, 300, out, accumulate=True)
+    torch.testing.assert_close(out, x.float().sum(0) + 1, rtol=1e-4, atol=1e-3)
+    w = torch.randn(70, 130, device=DEV)
+    wt = torch.empty(130, 70, device=DEV, dtype=torch.bfloat16)
+    nat.transpose_cast(w, wt)
+    torch.testing.assert_close(wt, w.t().bfloat16())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_embed_ln_fwd_bwd(dtype):
+    P, Lt, Tv, H, V = 4, 9, 5, 128, 50
+    T = Lt + Tv
+    g = torch.Generator(device="cpu").manual_seed(5)
+    ids = torch.randint(0, V, (P, Lt), generator=g).to(DEV)
+    ids[0, :3] = 0
+    tt = torch.zeros(P, Lt, dtype=torch.long, device=DEV)
+    word = torch.randn(V, H, generator=g).to(DEV)
+    pos = torch.randn(20, H, generator=g).to(DEV)
+    typ = torch.randn(1, H, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(H, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(H, generator=g)).to(DEV)
+    joint = torch.zeros(P, T, H, device=DEV, dtype=dtype)
+    mean = torch.empty(P * Lt, device=DEV)
+    rstd = torch.empty(P * Lt, device=DEV)
+    nat.embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gam, bet, 1e-12, joint, T * H, mean, rstd)
+    w_, p_, t_, g_, b_ = (x.clone().requires_grad_(True) for x in (word, pos, typ, gam, bet))
+    posid = torch.arange(Lt, device=DEV)[None].expand(P, Lt)
+    e = (torch.nn.functional.embedding(ids, w_, padding_idx=0)
+         + torch.nn.functional.embedding(posid, p_, padding_idx=0)
+         + torch.nn.functional.embedding(tt, t_, padding_idx=0))
+    ref = torch.nn.functional.layer_norm(e, (H,), g_, b_, 1e-12)
+    _close(joint[:, :Lt], ref, dtype)
+    dj = torch.randn(P, T, H, generator=g).to(DEV, dtype)
+    dw, dp, dty = torch.zeros_like(word), torch.zeros_like(pos), torch.zeros_like(typ)
+    dg, db = torch.zeros_like(gam), torch.zeros_like(bet)
+    nat.embed_ln_bwd(P, Lt, H, ids, tt, word, pos, typ, gam, mean, rstd, dj, T * H, dw, dp, dty,
+                     dg, db)
+    rw, rp, rt, rg, rb = torch.autograd.grad(ref, (w_, p_, t_, g_, b_), dj[:, :Lt].float())
+    for a_, b2 in ((dw, rw), (dp, rp), (dty, rt), (dg, rg), (db, rb)):
+        _close(a_, b2, torch.float32, scale=10.0 if dtype == torch.float32 else 300.0)
+    assert dw.abs().sum() > 0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_vit_im2col_embed_fwd_bwd(dtype):
+    B, Nst, R, ps, W = 2, 3, 32, 8, 64
+    g = torch.Generator(device="cpu").manual_seed(6)
+    images = torch.randn(B, Nst, 3, R, R, generator=g).to(DEV)
+    pairs = torch.tensor([[[0, 1], [2, 0]], [[1, 2], [2, 1]]], device=DEV)
+    npair = 2
+    P = B * npair
+    gg = (R // ps) ** 2
+    ntok = 1 + 2 * gg
+    patches = torch.empty(P * 2 * gg, 3 * ps * ps, device=DEV, dtype=dtype)
+    nat.vit_im2col(B, Nst, npair, R, ps, images, pairs, patches)
+    imgs = images[torch.arange(B)[:, None, None].to(DEV), pairs].reshape(P * 2, 3, R, R)
+    ref_p = torch.nn.functional.unfold(imgs, ps, stride=ps).transpose(1, 2).reshape(P * 2 * gg, -1)
+    _close(patches, ref_p, dtype)
+    po = torch.randn(P * 2 * gg, W, generator=g).to(DEV, dtype)
+    cls = torch.randn(W, generator=g).to(DEV)
+    pos = torch.randn(gg + 1, W, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(W, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(W, generator=g)).to(DEV)
+    x = torch.empty(P * ntok, W, device=DEV, dtype=dtype)
+    y = torch.empty_like(x)
+    mean = torch.empty(P * ntok, device=DEV)
+    rstd = torch.empty_like(mean)
+    nat.vit_embed_fwd(P, ntok, W, gg, po, cls, pos, gam, bet, 1e-5, x, y, mean, rstd)
+    po_, c_, p_, g_, b_ = (t.float().clone().requires_grad_(True) for t in (po, cls, pos, gam, bet))
+    xx = torch.cat([c_.expand(P, 1, W), po_.view(P, 2 * gg, W)], 1)
+    pe = torch.cat([p_, p_[:gg]], 0)
+    ref = torch.nn.functional.layer_norm(xx + pe, (W,), g_, b_, 1e-5)
+    _close(y.view(P, ntok, W), ref, dtype, scale=2.0)
+    dy = torch.randn(P * ntok, W, generator=g).to(DEV, dtype)
+    dpo = torch.empty_like(po)
+    dcls, dpos = torch.zeros_like(cls), torch.zeros_like(pos)
+    dg, db = torch.zeros_like(gam), torch.zeros_like(bet)
+    nat.vit_embed_bwd(P, ntok, W, gg, dy, x, mean, rstd, gam, dpo, dcls, dpos, dg, db)
+    r = torch.autograd.grad(ref, (po_, c_, p_, g_, b_), dy.float().view(P, ntok, W))
+    _close(dpo, r[0], dtype, scale=2.0)
+    for a_, b2 in ((dcls, r[1]), (dpos, r[2]), (dg, r[3]), (db, r[4])):
+        _close(a_, b2, torch.float32, scale=10.0 if dtype == torch.float32 else 300.0)

@@ -1,0 +1,56 @@
+"""CPU checks: the product model exposes the reference's state-dict names and shapes (drop-in
+checkpoint interop) and the C-ABI library exports every declared symbol."""
+import re
+import os
+
+import pytest
+import torch
+
+from golden_util import FIXTURES, load_fixture
+from multimodal_sequencing_amd import model_zoo
+from multimodal_sequencing_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_state_dict_matches_reference(name):
+    meta, _, params = load_fixture(name)
+    m = model_zoo.build_from_golden(meta["config"], device="cpu")
+    sd = m.state_dict()
+    ref = {k: tuple(v) for k, v in meta["shapes"].items()}
+    ours = {k: tuple(v.shape) for k, v in sd.items()}
+    assert set(ours) == set(ref), (sorted(set(ours) - set(ref)), sorted(set(ref) - set(ours)))
+    for k in ref:
+        assert ours[k] == ref[k], k
+    # load_state_dict round trip through the flat buffers
+    m.load_state_dict(params)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, params[k]), k
+
+
+def test_param_views_share_flat_storage():
+    meta, _, _ = load_fixture("tiny")
+    m = model_zoo.build_from_golden(meta["config"], device="cpu")
+    st = m.bert.store
+    q = "encoder.layer.0.attention.self."
+    packed = st.packed([q + "query.weight", q + "key.weight", q + "value.weight"], "f32")
+    assert packed.data_ptr() == st.params[q + "query.weight"].data_ptr()
+    assert torch.equal(packed[:128], st.params[q + "query.weight"].data)
+    assert torch.equal(packed[256:], st.params[q + "value.weight"].data)
+    p = st.params[q + "key.weight"]
+    assert p.grad.data_ptr() == st.grad.data_ptr() + 4 * st.offsets[q + "key.weight"]
+
+
+def test_abi_exports_every_declared_symbol():
+    src = open(os.path.join(ROOT, "include", "mmseq.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    protos = re.findall(r"(?:mmseq_status|int64_t|const char\*)\s+(mmseq_\w+)\s*\(([^;]*?)\);", src,
+                        flags=re.S)
+    assert len(protos) >= 25
+    lib = _native.lib()  # loads without a GPU; no compute calls here
+    for name, args in protos:
+        assert hasattr(lib, name), name
+        n = 0 if args.strip() in ("void", "") else len(args.split(","))
+        assert len(_native._SIGS[name][1]) == n, name
+    assert lib.mmseq_version().startswith(b"mmseq")
