@@ -63,6 +63,15 @@ mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch,
                         float alpha, int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
                         mmseq_stream stream);
 
+/* Selects the LDS-DMA fast path when its preconditions hold (default on); 0 forces the generic
+ * kernel (used by tests to cover both). */
+void mmseq_gemm_set_fast(int enable);
+/* Registers a caller-owned device workspace for split-K partial slabs (fp32). With it, wgrad-shaped
+ * TN GEMMs (few output tiles, long K, plain fp32 accumulate) split K across workgroups and reduce
+ * the slabs in a fixed order (bitwise reproducible). The workspace must not be used concurrently
+ * by GEMMs on different streams. NULL disables split-K. */
+void mmseq_gemm_set_workspace(void* ws, int64_t bytes);
+
 /* ------------------------------------------------------------------------------------------
  * Fused multi-head attention over a packed QKV activation (lxrt/modeling.py:398-425 with the
  * additive key mask of :1537-1545 / :1071-1094; clip/model.py:219-221 nn.MultiheadAttention).

@@ -43,6 +43,8 @@ _SIGS = {
                                                        _vp, _vp, _c_i64, _c_i64, ctypes.c_float,
                                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                        _vp]),
+    "mmseq_gemm_set_fast": (None, [ctypes.c_int]),
+    "mmseq_gemm_set_workspace": (None, [_vp, _c_i64]),
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            ctypes.c_int, _vp]),
@@ -95,6 +97,18 @@ _SIGS = {
 EXPORTS = sorted(k for k in _SIGS)
 
 
+_ws = {}
+
+
+def ensure_gemm_workspace(device, nbytes=256 << 20):
+    """Allocate (once per device) and register the split-K slab workspace."""
+    key = str(device)
+    if key not in _ws:
+        _ws[key] = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+        lib().mmseq_gemm_set_workspace(_ws[key].data_ptr(), nbytes)
+    return _ws[key]
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -143,6 +157,8 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
          bias=None, act=0, aux=None, dact=None, resid=None, ldr=None, sR=0, alpha=1.0,
          accumulate=False):
     _dev(A, B, C)
+    if not _ws:
+        ensure_gemm_workspace(A.device)
     if lda is None:
         lda = M if trans else K
     if ldb is None:
@@ -154,6 +170,10 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
     _check(lib().mmseq_gemm(trans, M, N, K, batch, _p(A), lda, sA, _p(B), ldb, sB, _p(C), ldc, sC,
                             _p(bias), act, _p(aux), _p(dact), _p(resid), ldr, sR, alpha,
                             int(accumulate), dt(A), dt(C), _stream()), "mmseq_gemm")
+
+
+def gemm_set_fast(enable):
+    lib().mmseq_gemm_set_fast(int(enable))
 
 
 def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse):

@@ -34,6 +34,23 @@ template <> struct Elem<unsigned short> {
   static __device__ __forceinline__ void st(unsigned short* p, float v) { *p = f2bf(v); }
 };
 
+// 4 contiguous elements <-> f32x4 (8-byte bf16 / 16-byte f32 accesses; caller guarantees alignment)
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  static __device__ __forceinline__ f32x4 ld(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+  static __device__ __forceinline__ void st(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+};
+template <> struct Vec4<unsigned short> {
+  static __device__ __forceinline__ f32x4 ld(const unsigned short* p) {
+    u16x4 u = *reinterpret_cast<const u16x4*>(p);
+    return (f32x4){bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3])};
+  }
+  static __device__ __forceinline__ void st(unsigned short* p, f32x4 v) {
+    u16x4 u = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    *reinterpret_cast<u16x4*>(p) = u;
+  }
+};
+
 // --- wave64 reductions ---
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -31,17 +31,40 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
   }
 }
 
-constexpr int CS_ROWS = 512;
-template <typename T>
+constexpr int CS_ROWS = 256;
+// partial column sums over CS_ROWS rows: lane owns 8 columns (16-byte bf16 loads when VEC),
+// the 4 waves of the block stride over the rows and are combined through LDS.
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(int rows, int cols, const T* __restrict__ x,
                                                              int64_t ldx, float* __restrict__ ws) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + lane * 8;
   const int r0 = blockIdx.y * CS_ROWS;
   const int r1 = min(rows, r0 + CS_ROWS);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += Elem<T>::ld(x + (int64_t)r * ldx + c);
-  ws[(int64_t)blockIdx.y * cols + c] = s;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = r0 + wave; r < r1; r += 4) {
+    const T* p = x + (int64_t)r * ldx + c0;
+    if (VEC && c0 + 8 <= cols) {
+      f32x4 a = Vec4<T>::ld(p), b = Vec4<T>::ld(p + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += a[e];
+        acc[4 + e] += b[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c0 + e < cols) acc[e] += Elem<T>::ld(p + e);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[wave][lane * 8 + e] = acc[e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = blockIdx.x * 512 + i;
+    if (c < cols) ws[(int64_t)blockIdx.y * cols + c] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
 }
 __global__ __launch_bounds__(256) void colsum_final_kernel(int nb, int cols, const float* __restrict__ ws,
                                                            float* __restrict__ out, int acc) {
@@ -171,13 +194,24 @@ extern "C" mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int nb = (rows + CS_ROWS - 1) / CS_ROWS;
   if (nb > 0) {
-    dim3 grid((cols + 255) / 256, nb);
-    if (dt == MMSEQ_F32)
-      hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, s, rows, cols,
-                         (const float*)x, ldx, ws);
-    else
-      hipLaunchKernelGGL(colsum_partial_kernel<unsigned short>, grid, dim3(256), 0, s, rows, cols,
-                         (const unsigned short*)x, ldx, ws);
+    dim3 grid((cols + 511) / 512, nb);
+    const int esz = dt == MMSEQ_F32 ? 4 : 2;
+    const bool vec = ((uintptr_t)x % 16) == 0 && ldx % 8 == 0 && (8 * esz) % 16 == 0;
+    if (dt == MMSEQ_F32) {
+      if (vec)
+        hipLaunchKernelGGL((colsum_partial_kernel<float, true>), grid, dim3(256), 0, s, rows, cols,
+                           (const float*)x, ldx, ws);
+      else
+        hipLaunchKernelGGL((colsum_partial_kernel<float, false>), grid, dim3(256), 0, s, rows,
+                           cols, (const float*)x, ldx, ws);
+    } else {
+      if (vec)
+        hipLaunchKernelGGL((colsum_partial_kernel<unsigned short, true>), grid, dim3(256), 0, s,
+                           rows, cols, (const unsigned short*)x, ldx, ws);
+      else
+        hipLaunchKernelGGL((colsum_partial_kernel<unsigned short, false>), grid, dim3(256), 0, s,
+                           rows, cols, (const unsigned short*)x, ldx, ws);
+    }
   }
   hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, nb, cols, ws,
                      out, accumulate);

@@ -17,6 +17,11 @@
 // previous tile) -> LDS after the barrier (the async-STAGE split of the guide, T14).
 #include "common.h"
 
+static int g_disable_fast = 0;  // test hook: force the generic kernel
+// caller-provided split-K slab workspace (mmseq_gemm_set_workspace); stream-ordered use only
+static float* g_slab = nullptr;
+static int64_t g_slab_bytes = 0;
+
 namespace {
 
 constexpr int BM = 128, BN = 128, NT_THREADS = 256;
@@ -40,6 +45,7 @@ struct GemmArgs {
   void* C; int64_t ldc, sC;
   const float* bias; int act; void* aux; const void* dact; const void* resid; int64_t ldr, sR;
   float alpha; int accumulate; int vec_ok; int vec_c;
+  int splitk; int kchunk; float* slab;  // split-K (TN wgrad): partial slabs [splitk][M][N] f32
 };
 
 template <typename TI, bool TRANS>
@@ -305,9 +311,210 @@ hipError_t launch(int trans, const GemmArgs& a, int batch, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// =============================================================================================
+// Fast path (bf16, both layouts): LDS-DMA staging (buffer_load ... lds, 16 B per lane) into a
+// two-stage double buffer, one barrier per 64-deep K-step, XOR-swizzled lane-linear LDS images
+// (swizzle applied to the per-lane SOURCE offset, guide rule 21), XCD-aware block order (T1).
+// Buffer resources give free zero-fill past the operand's last row (M/N edge for NT, K tail for
+// TN). Preconditions (checked on the host): NT needs K % 64 == 0; TN needs M % 8 == 0 and
+// N % 8 == 0; all leading dimensions multiples of 8, pointers 16-byte aligned.
+//   NT image: [128 rows][64 k], 128-B rows, chunk' = chunk ^ ((row >> 1) & 7)  -> conflict-free
+//             16-B row reads for the 16x16x32 operand (every 16-lane group hits 16 slots)
+//   TN image: [64 k][128 m], 256-B rows, chunk' = chunk ^ ((row & 7) << 1)     -> conflict-free
+//             ds_read_b64_tr_b16 (each 32-lane half reads 8 rows x 2 chunks = 16 slots)
+// =============================================================================================
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  uint32_t n = bytes <= 0 ? 0u : (bytes >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+
+__device__ __forceinline__ void dma16(rsrc_t r, unsigned short* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMSEQ_LDS void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <bool TRANS>
+__device__ __forceinline__ bf16x8_t frag_swz(const unsigned short* s, int rb, int ks, int lane) {
+  if (!TRANS) {
+    const int rr = rb + (lane & 15), c = ks * 4 + (lane >> 4);
+    const unsigned short* p = s + rr * 64 + ((c ^ ((rr >> 1) & 7)) << 3);
+    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(p));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int r = ks * 32 + 4 * g + q, col = rb + 4 * pp;
+    const unsigned short* a0 = s + r * 128 + (((col >> 3) ^ ((r & 7) << 1)) << 3) + (col & 7);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(a0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(a0 + 16 * 128));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+// issue this wave's 4 LDS-DMA pieces of one 128 x 64 operand tile
+template <bool TRANS>
+__device__ __forceinline__ void stage_operand(rsrc_t r, int64_t ld, int k0, unsigned short* s,
+                                              int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int inst = wave * 4 + i;
+    uint32_t voff;
+    if (!TRANS) {
+      const int row = inst * 8 + (lane >> 3), cp = lane & 7;
+      const int c = cp ^ ((row >> 1) & 7);
+      voff = (uint32_t)(((int64_t)row * ld + k0 + c * 8) * 2);
+    } else {
+      const int row = inst * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ ((row & 7) << 1);
+      voff = (uint32_t)(((int64_t)row * ld + c * 8) * 2);  // base already advanced to k0
+    }
+    dma16(r, s + inst * 512, voff);
+  }
+}
+
+template <typename TO, bool TRANS>
+__global__ __launch_bounds__(256, 2) void gemm_fast_kernel(GemmArgs a, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * 128 * 64];  // 64 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  // XCD-aware bijective remap: blocks that share an A panel run on one XCD (one L2)
+  const int nwg = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int Lr = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int tm = Lr / tiles_n, tn = Lr % tiles_n;
+  const int m0 = tm * 128, n0 = tn * 128;
+  const int split = a.splitk > 1 ? blockIdx.y : 0;
+  const int b = a.splitk > 1 ? 0 : blockIdx.y;
+  const int kbeg = split * a.kchunk;
+  const int Kend = a.splitk > 1 ? min(a.K, kbeg + a.kchunk) : a.K;
+  const unsigned short* A = reinterpret_cast<const unsigned short*>(a.A) + (int64_t)b * a.sA;
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(a.B) + (int64_t)b * a.sB;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (Kend - kbeg + 63) / 64;
+  rsrc_t ra, rb;
+  if (!TRANS) {
+    ra = make_rsrc(A + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
+    rb = make_rsrc(B + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
+  }
+  auto issue = [&](int kt, int stg) {
+    unsigned short* sA = smem + stg * 16384;
+    unsigned short* sB = sA + 8192;
+    const int k0 = kbeg + kt * 64;
+    if (!TRANS) {
+      stage_operand<false>(ra, a.lda, k0, sA, wave, lane);
+      stage_operand<false>(rb, a.ldb, k0, sB, wave, lane);
+    } else {
+      // rows k >= K fall outside the descriptor -> zero-filled
+      rsrc_t ta = make_rsrc(A + (int64_t)k0 * a.lda + m0,
+                            ((int64_t)(Kend - k0 - 1) * a.lda + (a.M - m0)) * 2);
+      rsrc_t tb = make_rsrc(B + (int64_t)k0 * a.ldb + n0,
+                            ((int64_t)(Kend - k0 - 1) * a.ldb + (a.N - n0)) * 2);
+      stage_operand<true>(ta, a.lda, k0, sA, wave, lane);
+      stage_operand<true>(tb, a.ldb, k0, sB, wave, lane);
+    }
+  };
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const unsigned short* sA = smem + cur * 16384;
+    const unsigned short* sB = sA + 8192;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = frag_swz<TRANS>(sA, wr * 64 + i * 16, ks, lane);
+        fb[i] = frag_swz<TRANS>(sB, wc * 64 + i * 16, ks, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int g = lane >> 4, ii = lane & 15;
+  if (a.splitk > 1) {  // raw fp32 partial slab, reduced (deterministically) by splitk_reduce
+    float* slab = a.slab + (int64_t)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int m = m0 + wr * 64 + i * 16 + ii;
+        int n = n0 + wc * 64 + j * 16 + 4 * g;
+        if (m < a.M && n < a.N)  // N % 8 == 0 on this path: n..n+3 all in range
+          *reinterpret_cast<f32x4*>(slab + (int64_t)m * a.N + n) = acc[i][j];
+      }
+    return;
+  }
+  TO* C = reinterpret_cast<TO*>(a.C) + (int64_t)b * a.sC;
+  const TO* resid = a.resid ? reinterpret_cast<const TO*>(a.resid) + (int64_t)b * a.sR : nullptr;
+  TO* aux = a.aux ? reinterpret_cast<TO*>(a.aux) + (int64_t)b * a.sC : nullptr;
+  const TO* dact = a.dact ? reinterpret_cast<const TO*>(a.dact) + (int64_t)b * a.sC : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m = m0 + wr * 64 + i * 16 + ii;
+      int n = n0 + wc * 64 + j * 16 + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epilogue4<TO>(a, C, resid, aux, dact, m, n, v);
+    }
+}
+
+// C[m][n] (+)= sum_s slab[s][m][n], fixed order (bitwise reproducible)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S, const float* __restrict__ slab,
+                                                            float* __restrict__ C, int64_t ldc,
+                                                            int accumulate) {
+  const int64_t total4 = (int64_t)M * N / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total4; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 4;
+    const int m = e / N, n = e % N;
+    f32x4 v = *reinterpret_cast<const f32x4*>(slab + e);
+    for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(slab + (int64_t)s * M * N + e);
+    float* cp = C + (int64_t)m * ldc + n;
+    if (accumulate) v += *reinterpret_cast<const f32x4*>(cp);
+    *reinterpret_cast<f32x4*>(cp) = v;
+  }
+}
+
+template <typename TO>
+hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s) {
+  const int tiles_m = (a.M + 127) / 128, tiles_n = (a.N + 127) / 128;
+  dim3 grid(tiles_m * tiles_n, a.splitk > 1 ? a.splitk : batch);
+  if (trans)
+    hipLaunchKernelGGL((gemm_fast_kernel<TO, true>), grid, dim3(256), 0, s, a, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_fast_kernel<TO, false>), grid, dim3(256), 0, s, a, tiles_n);
+  return hipGetLastError();
+}
+
 inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 }  // namespace
+
+extern "C" void mmseq_gemm_set_fast(int enable) { g_disable_fast = !enable; }
+
+extern "C" void mmseq_gemm_set_workspace(void* ws, int64_t bytes) {
+  g_slab = reinterpret_cast<float*>(ws);
+  g_slab_bytes = ws ? bytes : 0;
+}
 
 extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, const void* A,
                                    int64_t lda, int64_t strideA, const void* B, int64_t ldb,
@@ -345,7 +552,40 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   a.vec_c = ((uintptr_t)C % (vc * esz) == 0) && ldc % vc == 0 && strideC % vc == 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
-  if (in_dtype == MMSEQ_BF16 && out_dtype == MMSEQ_BF16)
+  const bool fast_ok = in_dtype == MMSEQ_BF16 && a.vec_ok && !g_disable_fast &&
+                       (trans ? (M % 8 == 0 && N % 8 == 0) : (K % 64 == 0)) &&
+                       (int64_t)M * N >= 128 * 128;
+  a.splitk = 1; a.kchunk = K; a.slab = nullptr;
+  if (fast_ok) {
+    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    const bool plain = !bias && !act && !aux_out && !dact_aux && !resid && alpha == 1.0f &&
+                       out_dtype == MMSEQ_F32 && batch == 1 && ldc % 4 == 0 && al16(C);
+    int S = 1;
+    if (trans && plain && g_slab && tiles < 512) {
+      S = (1024 + tiles - 1) / tiles;
+      const int maxS = K / (64 * 16);  // keep >= 16 K-steps per split
+      if (S > maxS) S = maxS;
+      while (S > 1 && (int64_t)S * M * N * 4 > g_slab_bytes) --S;
+    }
+    if (S > 1) {
+      a.splitk = S;
+      a.kchunk = ((K + S - 1) / S + 63) / 64 * 64;
+      S = (K + a.kchunk - 1) / a.kchunk;
+      a.splitk = S;
+      a.slab = g_slab;
+      e = launch_fast<float>(trans, a, 1, s);
+      if (e == hipSuccess) {
+        int64_t t4 = (int64_t)M * N / 4;
+        unsigned blocks = (unsigned)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, M, N, S, g_slab,
+                           (float*)C, ldc, accumulate);
+        e = hipGetLastError();
+      }
+    } else {
+      e = out_dtype == MMSEQ_BF16 ? launch_fast<unsigned short>(trans, a, batch, s)
+                                  : launch_fast<float>(trans, a, batch, s);
+    }
+  } else if (in_dtype == MMSEQ_BF16 && out_dtype == MMSEQ_BF16)
     e = launch<unsigned short, unsigned short>(trans, a, batch, s);
   else if (in_dtype == MMSEQ_BF16 && out_dtype == MMSEQ_F32)
     e = launch<unsigned short, float>(trans, a, batch, s);

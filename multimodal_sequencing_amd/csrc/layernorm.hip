@@ -3,18 +3,48 @@
 // clip/model.py:190-196 (fp32 LayerNorm, eps 1e-5); berson/encoder.py:16,42, neural.py:25 (1e-6).
 // Rows are addressed through mmseq_rows (two-level strides) so the kernels can read / write the
 // text or the visual half of the joint [P][T][H] activation in place (the fused concat).
+// Lane l owns columns j*256 + 4l .. +3 (j < 4): 8-byte (bf16) / 16-byte (f32) accesses when the
+// row layout allows it (VEC), scalar otherwise; cols <= 1024.
 #include "common.h"
 
 namespace {
 
-constexpr int MAXV = 16;  // cols <= 64 * 16 = 1024
-constexpr int RPB = 64;   // rows per workgroup in bwd (dgamma/dbeta partial granularity)
+constexpr int MAXJ = 4;   // 4 x 256 columns
+constexpr int RPB = 128;  // rows per workgroup in bwd (dgamma/dbeta partial granularity)
 
 __device__ __forceinline__ int64_t row_off(const mmseq_rows& l, int64_t r) {
   return (r / l.rpb) * l.bstride + (r % l.rpb) * l.ld;
 }
 
-template <typename TX, typename TY>
+template <typename T, bool VEC>
+__device__ __forceinline__ f32x4 ld4(const T* p, int c, int cols) {
+  if (VEC) {
+    if (c < cols) return Vec4<T>::ld(p + c);
+    return (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = c + e < cols ? Elem<T>::ld(p + c + e) : 0.f;
+  return v;
+}
+template <typename T, bool VEC>
+__device__ __forceinline__ void st4(T* p, int c, int cols, f32x4 v) {
+  if (VEC) {
+    if (c < cols) Vec4<T>::st(p + c, v);
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (c + e < cols) Elem<T>::st(p + c + e, v[e]);
+}
+__device__ __forceinline__ f32x4 ldp(const float* p, int c, int cols) {
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = c + e < cols ? p[c + e] : 0.f;
+  return v;
+}
+
+template <typename TX, typename TY, bool VEC>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const TX* __restrict__ x,
                                                      mmseq_rows xl, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
@@ -25,28 +55,32 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const TX* xr = x + row_off(xl, r);
-  float v[MAXV];
+  f32x4 v[MAXJ];
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int c = j * 64 + lane;
-    v[j] = c < cols ? Elem<TX>::ld(xr + c) : 0.f;
-    s += v[j];
+  for (int j = 0; j < MAXJ; ++j) {
+    v[j] = ld4<TX, VEC>(xr, j * 256 + lane * 4, cols);
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
   }
   const float mu = wave_sum(s) / cols;
   float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int c = j * 64 + lane;
-    float d = c < cols ? v[j] - mu : 0.f;
-    q += d * d;
-  }
+  for (int j = 0; j < MAXJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float d = (j * 256 + lane * 4 + e < cols) ? v[j][e] - mu : 0.f;
+      q += d * d;
+    }
   const float rs = rsqrtf(wave_sum(q) / cols + eps);
   TY* yr = y + row_off(yl, r);
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int c = j * 64 + lane;
-    if (c < cols) Elem<TY>::st(yr + c, (v[j] - mu) * rs * gamma[c] + beta[c]);
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c = j * 256 + lane * 4;
+    if (c >= cols) continue;
+    f32x4 g = ldp(gamma, c, cols), b = ldp(beta, c, cols), o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * g[e] + b[e];
+    st4<TY, VEC>(yr, c, cols, o);
   }
   if (lane == 0) {
     if (mean) mean[r] = mu;
@@ -56,7 +90,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
 
 // dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres)
 // per-block partial dgamma / dbeta -> ws[block][2][cols]
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                      mmseq_rows dyl, const T* __restrict__ x,
                                                      mmseq_rows xl, const float* __restrict__ mean,
@@ -67,30 +101,33 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
                                                      float* __restrict__ ws) {
   __shared__ float red[4][2][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pg[MAXV], pb[MAXV];
+  f32x4 pg[MAXJ], pb[MAXJ], gm[MAXJ];
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) pg[j] = pb[j] = 0.f;
+  for (int j = 0; j < MAXJ; ++j) {
+    pg[j] = pb[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    gm[j] = ldp(gamma, j * 256 + lane * 4, cols);
+  }
   const int64_t rbeg = (int64_t)blockIdx.x * RPB;
   for (int64_t r = rbeg + wave; r < rbeg + RPB && r < rows; r += 4) {
     const T* xr = x + row_off(xl, r);
     const T* dyr = dy + row_off(dyl, r);
     const float mu = mean[r], rs = rstd[r];
-    float xh[MAXV], gdy[MAXV];
+    f32x4 xh[MAXJ], gdy[MAXJ];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAXV; ++j) {
-      int c = j * 64 + lane;
-      if (c < cols) {
-        float xv = (Elem<T>::ld(xr + c) - mu) * rs;
-        float d = Elem<T>::ld(dyr + c);
-        xh[j] = xv;
-        gdy[j] = d * gamma[c];
-        pg[j] += d * xv;
-        pb[j] += d;
-        s1 += gdy[j];
-        s2 += gdy[j] * xv;
-      } else {
-        xh[j] = gdy[j] = 0.f;
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c = j * 256 + lane * 4;
+      f32x4 xv = ld4<T, VEC>(xr, c, cols), d = ld4<T, VEC>(dyr, c, cols);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = c + e < cols;
+        float xn = in ? (xv[e] - mu) * rs : 0.f;
+        xh[j][e] = xn;
+        gdy[j][e] = d[e] * gm[j][e];
+        pg[j][e] += d[e] * xn;
+        pb[j][e] += d[e];
+        s1 += gdy[j][e];
+        s2 += gdy[j][e] * xn;
       }
     }
     s1 = wave_sum(s1) / cols;
@@ -98,23 +135,30 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
     T* dxr = dx + row_off(dxl, r);
     const T* drr = dres ? dres + row_off(dresl, r) : nullptr;
 #pragma unroll
-    for (int j = 0; j < MAXV; ++j) {
-      int c = j * 64 + lane;
-      if (c < cols) {
-        float v = rs * (gdy[j] - s1 - xh[j] * s2);
-        if (drr) v += Elem<T>::ld(drr + c);
-        Elem<T>::st(dxr + c, v);
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c = j * 256 + lane * 4;
+      if (c >= cols) continue;
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rs * (gdy[j][e] - s1 - xh[j][e] * s2);
+      if (drr) {
+        f32x4 dr = ld4<T, VEC>(drr, c, cols);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += dr[e];
       }
+      st4<T, VEC>(dxr, c, cols, o);
     }
   }
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    int c = j * 64 + lane;
-    if (c < cols) {
-      red[wave][0][c] = pg[j];
-      red[wave][1][c] = pb[j];
+  for (int j = 0; j < MAXJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = j * 256 + lane * 4 + e;
+      if (c < cols) {
+        red[wave][0][c] = pg[j][e];
+        red[wave][1][c] = pb[j][e];
+      }
     }
-  }
   __syncthreads();
   for (int c = threadIdx.x; c < cols; c += 256) {
     float g = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
@@ -128,7 +172,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
 __global__ __launch_bounds__(256) void ln_reduce_kernel(int nb, int cols, const float* __restrict__ ws,
                                                         float* __restrict__ dg,
                                                         float* __restrict__ db) {
-  // grid.x = ceil(2*cols / 64); each wave handles one (which, col) pair per lane-strided loop
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int idx = blockIdx.x * 64 + lane;  // 0 .. 2*cols-1
@@ -143,6 +186,10 @@ __global__ __launch_bounds__(256) void ln_reduce_kernel(int nb, int cols, const 
     float* dst = which == 0 ? dg : db;
     if (dst) dst[c] += t;
   }
+}
+
+bool rows_vec(const void* p, const mmseq_rows& l, int esz) {
+  return ((uintptr_t)p % (4 * esz)) == 0 && l.ld % 4 == 0 && l.bstride % 4 == 0;
 }
 
 }  // namespace
@@ -164,13 +211,18 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
   if (rows == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((rows + 3) / 4);
-#define LNF(TX, TY) \
-  hipLaunchKernelGGL((ln_fwd_kernel<TX, TY>), grid, dim3(256), 0, s, rows, cols, (const TX*)x, xl, \
-                     gamma, beta, eps, (TY*)y, yl, mean, rstd)
-  if (xd == MMSEQ_F32 && yd == MMSEQ_F32) LNF(float, float);
-  else if (xd == MMSEQ_F32 && yd == MMSEQ_BF16) LNF(float, unsigned short);
-  else if (xd == MMSEQ_BF16 && yd == MMSEQ_F32) LNF(unsigned short, float);
-  else LNF(unsigned short, unsigned short);
+  const bool vec = cols % 4 == 0 && rows_vec(x, xl, xd == MMSEQ_BF16 ? 2 : 4) &&
+                   rows_vec(y, yl, yd == MMSEQ_BF16 ? 2 : 4);
+#define LNF(TX, TY, V)                                                                           \
+  hipLaunchKernelGGL((ln_fwd_kernel<TX, TY, V>), grid, dim3(256), 0, s, rows, cols, (const TX*)x, \
+                     xl, gamma, beta, eps, (TY*)y, yl, mean, rstd)
+#define LNF2(TX, TY) \
+  if (vec) LNF(TX, TY, true); else LNF(TX, TY, false)
+  if (xd == MMSEQ_F32 && yd == MMSEQ_F32) { LNF2(float, float); }
+  else if (xd == MMSEQ_F32 && yd == MMSEQ_BF16) { LNF2(float, unsigned short); }
+  else if (xd == MMSEQ_BF16 && yd == MMSEQ_F32) { LNF2(unsigned short, float); }
+  else { LNF2(unsigned short, unsigned short); }
+#undef LNF2
 #undef LNF
   return mmseq_check_launch("layernorm_fwd");
 }
@@ -191,15 +243,19 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
   if (!dres) dresl = dxl;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int nb = (rows + RPB - 1) / RPB;
-  if (dtype == MMSEQ_F32)
-    hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(nb), dim3(256), 0, s, rows, cols,
-                       (const float*)dy, dyl, (const float*)x, xl, mean, rstd, gamma, (float*)dx,
-                       dxl, (const float*)dres, dresl, workspace);
-  else
-    hipLaunchKernelGGL((ln_bwd_kernel<unsigned short>), dim3(nb), dim3(256), 0, s, rows, cols,
-                       (const unsigned short*)dy, dyl, (const unsigned short*)x, xl, mean, rstd,
-                       gamma, (unsigned short*)dx, dxl, (const unsigned short*)dres, dresl,
-                       workspace);
+  const int esz = dtype == MMSEQ_BF16 ? 2 : 4;
+  const bool vec = cols % 4 == 0 && rows_vec(dy, dyl, esz) && rows_vec(x, xl, esz) &&
+                   rows_vec(dx, dxl, esz) && (!dres || rows_vec(dres, dresl, esz));
+#define LNB(T, V)                                                                                 \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy,  \
+                     dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl, \
+                     workspace)
+  if (dtype == MMSEQ_F32) {
+    if (vec) LNB(float, true); else LNB(float, false);
+  } else {
+    if (vec) LNB(unsigned short, true); else LNB(unsigned short, false);
+  }
+#undef LNB
   mmseq_status st = mmseq_check_launch("layernorm_bwd");
   if (st) return st;
   if (dgamma || dbeta) return ln_reduce_partials(nb, cols, workspace, dgamma, dbeta, s);

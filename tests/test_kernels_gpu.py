@@ -34,7 +34,9 @@ def _q(x, dtype):
 @pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 200, 136), (77, 96, 520), (1, 2, 768),
                                    (513, 768, 768)])
 @pytest.mark.parametrize("act", [0, 1, 2, 3, 4])
-def test_gemm_nt_epilogues(dtype, M, N, K, act):
+@pytest.mark.parametrize("fast", [True, False])
+def test_gemm_nt_epilogues(dtype, M, N, K, act, fast):
+    nat.gemm_set_fast(fast)
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + act)
     A = torch.randn(M, K, generator=g).to(DEV, dtype)
     Bm = torch.randn(N, K, generator=g).to(DEV, dtype) * 0.1
@@ -53,8 +55,11 @@ def test_gemm_nt_epilogues(dtype, M, N, K, act):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 96, 300), (768, 768, 1026), (2, 520, 77)])
-def test_gemm_tn_accumulate(dtype, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 96, 300), (768, 768, 1026), (2, 520, 77),
+                                   (768, 3072, 4100), (136, 264, 64)])
+@pytest.mark.parametrize("fast", [True, False])
+def test_gemm_tn_accumulate(dtype, M, N, K, fast):
+    nat.gemm_set_fast(fast)
     # dW[M][N] += sum_k dY[k][M] X[k][N]  (wgrad layout)
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     dY = torch.randn(K, M, generator=g).to(DEV, dtype)
@@ -68,6 +73,7 @@ def test_gemm_tn_accumulate(dtype, M, N, K):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_dact_and_batched(dtype):
+    nat.gemm_set_fast(True)
     g = torch.Generator(device="cpu").manual_seed(3)
     M, Nn, K, Bt = 96, 64, 128, 3
     A = torch.randn(Bt, M, K, generator=g).to(DEV, dtype)
@@ -79,6 +85,20 @@ def test_gemm_dact_and_batched(dtype):
     gz = torch.autograd.grad(torch.nn.functional.gelu(zz).sum(), zz)[0]
     ref = (A.float() @ Bm.float().t()) * gz
     _close(C, ref, dtype, scale=2.0)
+
+
+def test_gemm_fast_strided_batched():
+    # batched NT with a row stride > K and non-multiple-of-128 M (visn_fc into the joint rows)
+    nat.gemm_set_fast(True)
+    Bt, M, K, Nn, ldc = 3, 200, 128, 192, 192
+    g = torch.Generator(device="cpu").manual_seed(9)
+    A = torch.randn(Bt, M, K, generator=g).to(DEV, torch.bfloat16)
+    W = torch.randn(Nn, K, generator=g).to(DEV, torch.bfloat16)
+    C = torch.zeros(Bt, M + 50, Nn, device=DEV, dtype=torch.bfloat16)
+    nat.gemm(A, W, C[:, 50:], M, Nn, K, batch=Bt, sA=M * K, sC=(M + 50) * Nn)
+    ref = A.float() @ W.float().t()
+    _close(C[:, 50:], ref, torch.bfloat16, scale=2.0)
+    assert C[:, :50].abs().max().item() == 0
 
 
 def _attn_ref(qkv, P, T, heads, bias, scale):

@@ -45,7 +45,7 @@ def test_param_views_share_flat_storage():
 def test_abi_exports_every_declared_symbol():
     src = open(os.path.join(ROOT, "include", "mmseq.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    protos = re.findall(r"(?:mmseq_status|int64_t|const char\*)\s+(mmseq_\w+)\s*\(([^;]*?)\);", src,
+    protos = re.findall(r"(?:mmseq_status|int64_t|const char\*|void)\s+(mmseq_\w+)\s*\(([^;]*?)\);", src,
                         flags=re.S)
     assert len(protos) >= 25
     lib = _native.lib()  # loads without a GPU; no compute calls here
