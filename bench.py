@@ -145,7 +145,8 @@ def main():
 
     preset = model_zoo.PRESETS[args.config]
     model = model_zoo.build_preset(args.config, device=dev, dtype=torch.bfloat16, seed=0)
-    model.train()
+    model.train()  # dropout p = 0.1 at every reference site, counter-based masks
+    model.bert.dropout_seed = 1 + rank
     stores = model.stores()
     opt = FusedAdamW(stores, lr=5e-6, warmup=100)
     reducer = GradAllReduce(stores) if world > 1 else None
@@ -196,7 +197,8 @@ def main():
         "value": steps_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic (seeded token ids U[3,50265), N(0,1) 224x224 images), random-init weights",
+        "data": "synthetic (seeded token ids U[3,50265), N(0,1) 224x224 images), random-init "
+                "weights, train mode (dropout 0.1)",
         "config": {"workload": f"{args.config}: ViT-B/16 + 12x768 joint encoder + BERSON, "
                                f"N={Nst} steps, {Pst} pairs/story, pair seq {Lt}+{Tv}={Lt + Tv}",
                    "global_batch": args.batch * world, "stories_per_gpu": args.batch,

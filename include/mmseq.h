@@ -38,6 +38,15 @@ typedef enum {
   MMSEQ_ACT_GELU_TANH = 4
 } mmseq_act;
 
+/* Dropout (train mode). Counter-based: keep(idx) = hash(seed, stream, idx) >= p * 2^24, kept
+ * values scaled by 1/(1-p); the same (seed, stream) regenerates the mask in the backward, so no
+ * mask is ever stored. A NULL pointer or p == 0 means no dropout. */
+typedef struct {
+  float p;
+  uint32_t stream;
+  uint64_t seed;
+} mmseq_dropout;
+
 const char* mmseq_last_error(void);
 const char* mmseq_version(void);
 
@@ -51,6 +60,7 @@ const char* mmseq_version(void);
  *   epilogue, in order:  v += bias[n] (f32, optional)
  *                        if dact_aux: v *= act'(dact_aux[m][n])          (backward through act)
  *                        else if act: aux_out[m][n] = v (optional); v = act(v)
+ *                        v = dropout(v) (optional, idx = (b*M + m)*N + n)
  *                        v += resid[m][n] (optional)   ;   if accumulate: v += C[m][n]
  *   A, B share in_dtype; C, resid, aux_out, dact_aux share out_dtype (aux ld = ldc).
  * ------------------------------------------------------------------------------------------ */
@@ -61,10 +71,12 @@ mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch,
                         const float* bias, int act, void* aux_out, const void* dact_aux,
                         const void* resid, int64_t ldr, int64_t strideR,
                         float alpha, int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
-                        mmseq_stream stream);
+                        const mmseq_dropout* drop, mmseq_stream stream);
 
-/* Selects the LDS-DMA fast path when its preconditions hold (default on); 0 forces the generic
- * kernel (used by tests to cover both). */
+/* Kernel selection (tests and microbenchmarks cover every variant): 1 = default (256 x 256 NT
+ * kernel for large problems, 128 x 128 double-buffer otherwise), 2 = 128 x 128 double-buffer,
+ * 3 = 128 x 128 ring only, 4 = 256 x 256 NT for every eligible NT problem, 0 = generic
+ * register-staged kernel only. */
 void mmseq_gemm_set_fast(int enable);
 /* Registers a caller-owned device workspace for split-K partial slabs (fp32). With it, wgrad-shaped
  * TN GEMMs (few output tiles, long K, plain fp32 accumulate) split K across workgroups and reduce
@@ -80,35 +92,41 @@ void mmseq_gemm_set_workspace(void* ws, int64_t bytes);
  *   key_bias: [P][T] f32 additive (0 or -10000), or NULL.  out row: out + (p*T+t)*ld_out + h*64.
  *   lse: [P][heads][T] f32 (log-sum-exp of the scaled, biased scores), written by fwd.
  * bwd: delta workspace [P][heads][T] f32; dqkv has the same packed layout as qkv (ld_dqkv).
+ * drop: attention-probability dropout (lxrt:421), idx = ((p*heads + h)*T + q)*T + k.
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, void* out, int64_t ld_out, float* lse,
-                            mmseq_dtype dtype, mmseq_stream stream);
+                            mmseq_dtype dtype, const mmseq_dropout* drop, mmseq_stream stream);
 mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, const void* out, int64_t ld_out, const void* dout,
                             int64_t ld_dout, const float* lse, float* delta, void* dqkv,
-                            int64_t ld_dqkv, mmseq_dtype dtype, mmseq_stream stream);
+                            int64_t ld_dqkv, mmseq_dtype dtype, const mmseq_dropout* drop,
+                            mmseq_stream stream);
 
 /* Small multi-head attention for the BERSON inter-sentence encoder (neural.py:98-235):
  * [B][T][heads*d] separate q/k/v tensors, T <= 64, d <= 128, fp32, key_bias [B][T] or NULL.
- * probs [B][heads][T][T] are saved by fwd for bwd. */
+ * probs [B][heads][T][T] (before dropout) are saved by fwd for bwd; drop = probability dropout
+ * (neural.py:221), idx = ((b*heads + h)*T + i)*T + j. */
 mmseq_status mmseq_small_attn_fwd(int B, int T, int heads, int d, const float* q, const float* k,
                                   const float* v, const float* key_bias, float scale, float* out,
-                                  float* probs, mmseq_stream stream);
+                                  float* probs, const mmseq_dropout* drop, mmseq_stream stream);
 mmseq_status mmseq_small_attn_bwd(int B, int T, int heads, int d, const float* q, const float* k,
                                   const float* v, const float* probs, const float* dout,
                                   float scale, float* dq, float* dk, float* dv,
-                                  mmseq_stream stream);
+                                  const mmseq_dropout* drop, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * LayerNorm over the last dim (cols), fp32 statistics (lxrt BertLayerNorm eps 1e-12:
  * :353,432,486,577; CLIP fp32 LayerNorm eps 1e-5: clip/model.py:190-196; BERSON eps 1e-6).
  * Row r lives at base + (r / rpb)*bstride + (r % rpb)*ld  (two-level strides let the kernels
  * read/write the text or visual half of the joint [P][T][H] buffer in place; rpb = rows
- * per batch).  bwd: dx = LN'(dy) (+ dres if non-NULL); dgamma/dbeta ACCUMULATE (+=) and need a
- * workspace of mmseq_layernorm_bwd_workspace(rows, cols) floats.
+ * per batch).  fwd: y = LN(x), then dropout(y) if drop_y (idx = r*cols + c).
+ * bwd: dy is first multiplied by drop_dy's mask (the fwd drop_y), dx = LN'(dy) (+ dres if
+ * non-NULL); if dx_drop, it also receives dx * drop_dx's mask (the gradient of a
+ * dropout(dense) + residual sum, idx = r*cols + c, same layout as dx). dgamma/dbeta ACCUMULATE
+ * (+=) and need a workspace of mmseq_layernorm_bwd_workspace(rows, cols) floats.
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   int64_t ld;       /* row stride (elements) inside a batch */
@@ -119,13 +137,16 @@ typedef struct {
 mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, mmseq_rows xl,
                                  const float* gamma, const float* beta, float eps, void* y,
                                  mmseq_rows yl, float* mean, float* rstd, mmseq_dtype x_dtype,
-                                 mmseq_dtype y_dtype, mmseq_stream stream);
+                                 mmseq_dtype y_dtype, const mmseq_dropout* drop_y,
+                                 mmseq_stream stream);
 int64_t mmseq_layernorm_bwd_workspace(int rows, int cols);
 mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
                                  const void* x, mmseq_rows xl, const float* mean,
                                  const float* rstd, const float* gamma, void* dx, mmseq_rows dxl,
                                  const void* dres, mmseq_rows dresl, float* dgamma, float* dbeta,
-                                 float* workspace, mmseq_dtype dtype, mmseq_stream stream);
+                                 float* workspace, mmseq_dtype dtype,
+                                 const mmseq_dropout* drop_dy, void* dx_drop,
+                                 const mmseq_dropout* drop_dx, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused text embedding + LayerNorm written straight into the joint buffer (BertEmbeddings,
@@ -133,18 +154,19 @@ mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows 
  *   e = word[ids] + pos[t] + type[tt];  joint row (p*ld_pair + t) = LN(e)   (eps as given)
  * bwd recomputes e, applies LN backward and scatters into dword/dpos/dtype (+=), skipping
  * row 0 of every table (padding_idx = 0 on all three, :347-349). dgamma/dbeta accumulate.
+ * drop: embedding dropout (:369) on the LN output, idx = (p*Lt + t)*H + c.
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* ids, const int64_t* tt,
                                 const float* word, const float* pos, const float* type,
                                 const float* gamma, const float* beta, float eps, void* joint,
                                 int64_t ld_pair, float* mean, float* rstd, mmseq_dtype dtype,
-                                mmseq_stream stream);
+                                const mmseq_dropout* drop, mmseq_stream stream);
 mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* ids, const int64_t* tt,
                                 const float* word, const float* pos, const float* type,
                                 const float* gamma, const float* mean, const float* rstd,
                                 const void* djoint, int64_t ld_pair, float* dword, float* dpos,
                                 float* dtype_tab, float* dgamma, float* dbeta, float* workspace,
-                                mmseq_dtype dtype, mmseq_stream stream);
+                                mmseq_dtype dtype, const mmseq_dropout* drop, mmseq_stream stream);
 int64_t mmseq_embed_ln_bwd_workspace(int P, int Lt, int H);
 
 /* ------------------------------------------------------------------------------------------
@@ -189,6 +211,10 @@ mmseq_status mmseq_act_fwd(int64_t n, int act, const void* x, void* y, mmseq_dty
                            mmseq_stream stream);
 mmseq_status mmseq_act_bwd(int64_t n, int act, const void* z, const void* dy, void* dz,
                            mmseq_dtype dtype, mmseq_stream stream);
+/* y[i] = x[i] * mask(i) (idx = i); also the backward of itself (the BERSON head's nn.Dropout
+ * sites: neural.py:31-32, encoder.py:28). y may alias x. */
+mmseq_status mmseq_dropout_apply(int64_t n, const void* x, void* y, mmseq_dtype dtype,
+                                 const mmseq_dropout* drop, mmseq_stream stream);
 /* sum of squares of n f32 values into out[0] (overwrite), two-pass deterministic */
 mmseq_status mmseq_sumsq(int64_t n, const float* x, float* out, float* workspace,
                          mmseq_stream stream);
@@ -233,17 +259,19 @@ mmseq_status mmseq_pointer_bwd(int B, int N, int H, const float* q, const float*
  * HierarchicalAttention span pooling (modeling_bert.py:703-741) without host loops:
  *   for pair p, span s in {0,1}: mask_s(t) = 1 for t in [1, sep0] (s=0) / [sep0+1, sep1] (s=1)
  *   a[p][s][t] = mask ? score[p][t] : -10000 ; probs = softmax_t(a); mix[p][s] = probs @ top[p]
- *   top rows: top + p*ld_pair + t*H. probs saved [P][2][Lt] f32 for bwd.
+ *   top rows: top + p*ld_pair + t*H. probs (before dropout) saved [P][2][Lt] f32 for bwd;
+ *   drop = probability dropout (:735), idx = (p*2 + s)*Lt + t.
  * bwd: dscore[p][t] = sum_s mask*probs*(dmix.top - sum_t' probs*dmix.top) (written);
  *      dtop[p][t] += probs^T dmix (accumulated in place)
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_span_pool_fwd(int P, int Lt, int H, const void* top, int64_t ld_pair,
                                  const float* score, const int64_t* sep, float* probs,
-                                 float* mix, mmseq_dtype dtype, mmseq_stream stream);
+                                 float* mix, mmseq_dtype dtype, const mmseq_dropout* drop,
+                                 mmseq_stream stream);
 mmseq_status mmseq_span_pool_bwd(int P, int Lt, int H, const void* top, int64_t ld_pair,
                                  const float* probs, const int64_t* sep, const float* dmix,
                                  float* dscore, void* dtop, mmseq_dtype dtype,
-                                 mmseq_stream stream);
+                                 const mmseq_dropout* drop, mmseq_stream stream);
 
 #ifdef __cplusplus
 }

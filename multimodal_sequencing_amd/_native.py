@@ -28,6 +28,23 @@ def rows(ld, bstride=0, rpb=1 << 62):
     return Rows(ld, bstride, rpb)
 
 
+class Dropout(ctypes.Structure):
+    """mmseq_dropout: counter-based mask keyed by (seed, stream, element index)."""
+    _fields_ = [("p", ctypes.c_float), ("stream", ctypes.c_uint32), ("seed", ctypes.c_uint64)]
+
+
+_dp = ctypes.POINTER(Dropout)
+
+
+def drop(p, stream, seed):
+    """A dropout descriptor, or None when p == 0 (the kernels then skip the mask)."""
+    return Dropout(p, stream & 0xFFFFFFFF, seed & 0xFFFFFFFFFFFFFFFF) if p > 0 else None
+
+
+def _d(d):
+    return None if d is None else ctypes.byref(d)
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -42,32 +59,32 @@ _SIGS = {
                                                        _vp, _c_i64, _c_i64, _vp, ctypes.c_int, _vp,
                                                        _vp, _vp, _c_i64, _c_i64, ctypes.c_float,
                                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                                       _vp]),
+                                                       _dp, _vp]),
     "mmseq_gemm_set_fast": (None, [ctypes.c_int]),
     "mmseq_gemm_set_workspace": (None, [_vp, _c_i64]),
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
-                                                           ctypes.c_int, _vp]),
+                                                           ctypes.c_int, _dp, _vp]),
     "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            _c_i64, _vp, _vp, _vp, _c_i64,
-                                                           ctypes.c_int, _vp]),
+                                                           ctypes.c_int, _dp, _vp]),
     "mmseq_small_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 4 + [ctypes.c_float, _vp,
-                                                                             _vp, _vp]),
+                                                                             _vp, _dp, _vp]),
     "mmseq_small_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float, _vp,
-                                                                             _vp, _vp, _vp]),
+                                                                             _vp, _vp, _dp, _vp]),
     "mmseq_layernorm_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, _vp,
                                            ctypes.c_float, _vp, Rows, _vp, _vp, ctypes.c_int,
-                                           ctypes.c_int, _vp]),
+                                           ctypes.c_int, _dp, _vp]),
     "mmseq_layernorm_bwd_workspace": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
     "mmseq_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
                                            _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
-                                           ctypes.c_int, _vp]),
+                                           ctypes.c_int, _dp, _vp, _dp, _vp]),
     "mmseq_embed_ln_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 7 + [ctypes.c_float, _vp,
                                                                            _c_i64, _vp, _vp,
-                                                                           ctypes.c_int, _vp]),
+                                                                           ctypes.c_int, _dp, _vp]),
     "mmseq_embed_ln_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 9 + [_c_i64] + [_vp] * 6 +
-                           [ctypes.c_int, _vp]),
+                           [ctypes.c_int, _dp, _vp]),
     "mmseq_embed_ln_bwd_workspace": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_vit_im2col": (ctypes.c_int, [ctypes.c_int] * 5 + [_vp, _vp, _vp, ctypes.c_int, _vp]),
     "mmseq_vit_embed_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float] +
@@ -82,6 +99,7 @@ _SIGS = {
     "mmseq_colsum_workspace": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
     "mmseq_act_fwd": (ctypes.c_int, [_c_i64, ctypes.c_int, _vp, _vp, ctypes.c_int, _vp]),
     "mmseq_act_bwd": (ctypes.c_int, [_c_i64, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_dropout_apply": (ctypes.c_int, [_c_i64, _vp, _vp, ctypes.c_int, _dp, _vp]),
     "mmseq_sumsq": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp]),
     "mmseq_sumsq_workspace": (ctypes.c_int64, [_c_i64]),
     "mmseq_adamw": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp] + [ctypes.c_float] * 5 +
@@ -89,9 +107,9 @@ _SIGS = {
     "mmseq_pointer_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 5 + [_vp] * 5 + [_vp]),
     "mmseq_pointer_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 14 + [_vp]),
     "mmseq_span_pool_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
-                                                                ctypes.c_int, _vp]),
+                                                                ctypes.c_int, _dp, _vp]),
     "mmseq_span_pool_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
-                                                                _vp, ctypes.c_int, _vp]),
+                                                                _vp, ctypes.c_int, _dp, _vp]),
 }
 
 EXPORTS = sorted(k for k in _SIGS)
@@ -155,7 +173,7 @@ def _dev(*ts):
 # ------------------------------------------------------------------------------------------------
 def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA=0, sB=0, sC=0,
          bias=None, act=0, aux=None, dact=None, resid=None, ldr=None, sR=0, alpha=1.0,
-         accumulate=False):
+         accumulate=False, drop=None):
     _dev(A, B, C)
     if not _ws:
         ensure_gemm_workspace(A.device)
@@ -169,68 +187,73 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
         ldr = ldc
     _check(lib().mmseq_gemm(trans, M, N, K, batch, _p(A), lda, sA, _p(B), ldb, sB, _p(C), ldc, sC,
                             _p(bias), act, _p(aux), _p(dact), _p(resid), ldr, sR, alpha,
-                            int(accumulate), dt(A), dt(C), _stream()), "mmseq_gemm")
+                            int(accumulate), dt(A), dt(C), _d(drop), _stream()), "mmseq_gemm")
 
 
 def gemm_set_fast(enable):
     lib().mmseq_gemm_set_fast(int(enable))
 
 
-def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse):
+def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse,
+             drop=None):
     _dev(qkv, out, lse)
     _check(lib().mmseq_attn_fwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
-                                scale, _p(out), ld_out, _p(lse), dt(qkv), _stream()),
+                                scale, _p(out), ld_out, _p(lse), dt(qkv), _d(drop), _stream()),
            "mmseq_attn_fwd")
 
 
 def attn_bwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, dout,
-             ld_dout, lse, delta, dqkv, ld_dqkv):
+             ld_dout, lse, delta, dqkv, ld_dqkv, drop=None):
     _check(lib().mmseq_attn_bwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
                                 scale, _p(out), ld_out, _p(dout), ld_dout, _p(lse), _p(delta),
-                                _p(dqkv), ld_dqkv, dt(qkv), _stream()), "mmseq_attn_bwd")
+                                _p(dqkv), ld_dqkv, dt(qkv), _d(drop), _stream()),
+           "mmseq_attn_bwd")
 
 
-def small_attn_fwd(B, T, heads, d, q, k, v, key_bias, scale, out, probs):
+def small_attn_fwd(B, T, heads, d, q, k, v, key_bias, scale, out, probs, drop=None):
     _check(lib().mmseq_small_attn_fwd(B, T, heads, d, _p(q), _p(k), _p(v), _p(key_bias), scale,
-                                      _p(out), _p(probs), _stream()), "mmseq_small_attn_fwd")
+                                      _p(out), _p(probs), _d(drop), _stream()),
+           "mmseq_small_attn_fwd")
 
 
-def small_attn_bwd(B, T, heads, d, q, k, v, probs, dout, scale, dq, dk, dv):
+def small_attn_bwd(B, T, heads, d, q, k, v, probs, dout, scale, dq, dk, dv, drop=None):
     _check(lib().mmseq_small_attn_bwd(B, T, heads, d, _p(q), _p(k), _p(v), _p(probs), _p(dout),
-                                      scale, _p(dq), _p(dk), _p(dv), _stream()),
+                                      scale, _p(dq), _p(dk), _p(dv), _d(drop), _stream()),
            "mmseq_small_attn_bwd")
 
 
-def layernorm_fwd(nrows, cols, x, xl, gamma, beta, eps, y, yl, mean, rstd):
+def layernorm_fwd(nrows, cols, x, xl, gamma, beta, eps, y, yl, mean, rstd, drop=None):
     _dev(x, y, gamma, beta)
     _check(lib().mmseq_layernorm_fwd(nrows, cols, _p(x), xl, _p(gamma), _p(beta), eps, _p(y), yl,
-                                     _p(mean), _p(rstd), dt(x), dt(y), _stream()),
+                                     _p(mean), _p(rstd), dt(x), dt(y), _d(drop), _stream()),
            "mmseq_layernorm_fwd")
 
 
 def layernorm_bwd(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl, dgamma,
-                  dbeta):
+                  dbeta, drop_dy=None, dx_drop=None, drop_dx=None):
     ws = torch.empty(lib().mmseq_layernorm_bwd_workspace(nrows, cols), dtype=torch.float32,
                      device=x.device)
     _check(lib().mmseq_layernorm_bwd(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
                                      _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
-                                     _p(dbeta), _p(ws), dt(x), _stream()), "mmseq_layernorm_bwd")
+                                     _p(dbeta), _p(ws), dt(x), _d(drop_dy), _p(dx_drop),
+                                     _d(drop_dx), _stream()), "mmseq_layernorm_bwd")
 
 
-def embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gamma, beta, eps, joint, ld_pair, mean, rstd):
+def embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gamma, beta, eps, joint, ld_pair, mean, rstd,
+                 drop=None):
     _check(lib().mmseq_embed_ln_fwd(P, Lt, H, _p(ids), _p(tt), _p(word), _p(pos), _p(typ),
                                     _p(gamma), _p(beta), eps, _p(joint), ld_pair, _p(mean),
-                                    _p(rstd), dt(joint), _stream()), "mmseq_embed_ln_fwd")
+                                    _p(rstd), dt(joint), _d(drop), _stream()), "mmseq_embed_ln_fwd")
 
 
 def embed_ln_bwd(P, Lt, H, ids, tt, word, pos, typ, gamma, mean, rstd, djoint, ld_pair, dword,
-                 dpos, dtyp, dgamma, dbeta):
+                 dpos, dtyp, dgamma, dbeta, drop=None):
     ws = torch.empty(lib().mmseq_embed_ln_bwd_workspace(P, Lt, H), dtype=torch.float32,
                      device=djoint.device)
     _check(lib().mmseq_embed_ln_bwd(P, Lt, H, _p(ids), _p(tt), _p(word), _p(pos), _p(typ),
                                     _p(gamma), _p(mean), _p(rstd), _p(djoint), ld_pair, _p(dword),
                                     _p(dpos), _p(dtyp), _p(dgamma), _p(dbeta), _p(ws),
-                                    dt(djoint), _stream()), "mmseq_embed_ln_bwd")
+                                    dt(djoint), _d(drop), _stream()), "mmseq_embed_ln_bwd")
 
 
 def vit_im2col(B, N, npair, R, ps, images, pairs, patches):
@@ -280,6 +303,11 @@ def act_bwd(z, dy, dz, act):
            "mmseq_act_bwd")
 
 
+def dropout(x, y, drop):
+    _check(lib().mmseq_dropout_apply(x.numel(), _p(x), _p(y), dt(x), _d(drop), _stream()),
+           "mmseq_dropout_apply")
+
+
 def sumsq(x, out):
     ws = torch.empty(lib().mmseq_sumsq_workspace(x.numel()), dtype=torch.float32, device=x.device)
     _check(lib().mmseq_sumsq(x.numel(), _p(x), _p(out), _p(ws), _stream()), "mmseq_sumsq")
@@ -304,12 +332,12 @@ def pointer_bwd(B, N, H, q, key, okey, w, logp, pointed, tgt_len, target, dnll, 
                                    _p(dokey), _p(dw), _p(dwb), _stream()), "mmseq_pointer_bwd")
 
 
-def span_pool_fwd(P, Lt, H, top, ld_pair, score, sep, probs, mix):
+def span_pool_fwd(P, Lt, H, top, ld_pair, score, sep, probs, mix, drop=None):
     _check(lib().mmseq_span_pool_fwd(P, Lt, H, _p(top), ld_pair, _p(score), _p(sep), _p(probs),
-                                     _p(mix), dt(top), _stream()), "mmseq_span_pool_fwd")
+                                     _p(mix), dt(top), _d(drop), _stream()), "mmseq_span_pool_fwd")
 
 
-def span_pool_bwd(P, Lt, H, top, ld_pair, probs, sep, dmix, dscore, dtop):
+def span_pool_bwd(P, Lt, H, top, ld_pair, probs, sep, dmix, dscore, dtop, drop=None):
     _check(lib().mmseq_span_pool_bwd(P, Lt, H, _p(top), ld_pair, _p(probs), _p(sep), _p(dmix),
-                                     _p(dscore), _p(dtop), dt(top), _stream()),
+                                     _p(dscore), _p(dtop), dt(top), _d(drop), _stream()),
            "mmseq_span_pool_bwd")

@@ -85,6 +85,9 @@ class BertForOrdering(nn.Module):
         self.device_ = torch.device(device)
         self.bert = inner_model
         self._maps = {}
+        self.hidden_dropout_prob = getattr(config, "hidden_dropout_prob", 0.1)  # :677
+        self.para_dropout = getattr(args, "para_dropout", 0.1)  # train.py:2014, :881
+        self._drops = K.EVAL
 
     # ------------------------------------------------------------------------------------
     def stores(self):
@@ -143,17 +146,22 @@ class BertForOrdering(nn.Module):
         mp = self._static_maps(N)
         if self.store.shadow_stale:  # transposed fp32 weight shadows for the head's dgrad GEMMs
             self.store.refresh_shadows()
+        D = self.bert.new_dropouts()
+        D.training = D.training and self.training
+        self._drops = D
+        ph = self.hidden_dropout_prob
         joint, Lt = self.bert.encode_joint(input_ids.reshape(P, Lt),
                                            attention_mask.reshape(P, Lt),
                                            token_type_ids.reshape(P, Lt),
                                            images if not self.bert.text_part else None,
-                                           pairs_list)
+                                           pairs_list, drops=D)
         top = joint[:, :Lt].float()  # lang_feats (:1289), fp32 for the head
         cls_pooled = top[:, 0]  # :1290
         # ---- HierarchicalAttention (:686-817) -------------------------------------------
         t = "two_level_encoder."
         score = self._lin(self._lin(top, t + "sentence_tran", act=K.TANH), t + "sentence_tran_2")
-        mix = K.SpanPoolFn.apply(top, score.view(P, Lt), sep_positions.reshape(P, 2).contiguous())
+        mix = K.SpanPoolFn.apply(top, score.view(P, Lt), sep_positions.reshape(P, 2).contiguous(),
+                                 D.site(ph, "span"))  # :735
         sample = mix.view(B, 2 * npair, H)[:, mp["slot"]].view(B, N, mp["E"], H)
         q2 = K.LinearFn.apply(sample, self._anchor, self.store, t + "linear_in_2.weight", None, 0)
         wts = torch.softmax(q2.view(B, N, mp["E"]), -1)
@@ -182,16 +190,22 @@ class BertForOrdering(nn.Module):
         x = top_vecs * mask[:, :, None]
         key_bias = ((1.0 - mask) * -10000.0).contiguous()  # neural.py:210-213 with mask = 1 - m
         heads = self.args.heads
+        D = self._drops
+        pd = self.para_dropout
         for i in range(self.args.inter_layers):
             b = f"encoder.transformer_inter.{i}."
             h = self._ln(x, b + "layer_norm", 1e-6) if i != 0 else x
             q = self._lin(h, b + "self_attn.linear_query")
             k = self._lin(h, b + "self_attn.linear_keys")
             v = self._lin(h, b + "self_attn.linear_values")
-            ctx = K.SmallAttnFn.apply(q, k, v, key_bias, heads)
-            out = self._lin(ctx, b + "self_attn.final_linear") + x
-            f = self._lin(self._lin(self._ln(out, b + "feed_forward.layer_norm", 1e-6),
-                                    b + "feed_forward.w_1", act=K.GELU_TANH), b + "feed_forward.w_2")
+            ctx = K.SmallAttnFn.apply(q, k, v, key_bias, heads, D.site(pd, "inter_att", i))
+            # encoder.py:28 and neural.py:31-33
+            out = K.dropout(self._lin(ctx, b + "self_attn.final_linear"),
+                            D.site(pd, "inter_ctx", i)) + x
+            inter = K.dropout(self._lin(self._ln(out, b + "feed_forward.layer_norm", 1e-6),
+                                        b + "feed_forward.w_1", act=K.GELU_TANH),
+                              D.site(pd, "inter_ff1", i))
+            f = K.dropout(self._lin(inter, b + "feed_forward.w_2"), D.site(pd, "inter_ff2", i))
             x = f + out
         return self._ln(x, "encoder.layer_norm", 1e-6)
 

@@ -39,6 +39,7 @@ struct AttnArgs {
   float* lse; float* delta;
   void* dqkv; int64_t ld_dqkv;
   void* o_w;  // fwd output
+  Drop drop;  // attention-probability dropout
 };
 
 // Stage rows [r0, r0+64) of one head's 64-wide slice into LDS tile s ([64][LD]); zero-fill >= T.
@@ -186,6 +187,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     l = l * alpha + rs;
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    if (a.drop.thr) {  // the normaliser l keeps the undropped probabilities (dropout after softmax)
+      const uint64_t rowi = (((uint64_t)p * a.heads + h) * T + (q0 + i)) * T + k0;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kb][r] *= drop_mul(a.drop, rowi + kb * 16 + 4 * g + r);
+    }
     if constexpr (sizeof(TI) == 2) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -325,8 +333,9 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         int qi = qs * 16 + 4 * g + r;
         float pv = __expf(s[qs][r] * a.scale + kbias - sL[qi]);
-        s[qs][r] = pv;
-        dp[qs][r] = pv * (dp[qs][r] - sD[qi]);
+        const float mul = drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + qb0 + qi) * T + mykey);
+        s[qs][r] = pv * mul;
+        dp[qs][r] = pv * (dp[qs][r] * mul - sD[qi]);
       }
     // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
     if constexpr (sizeof(TI) == 2) {
@@ -449,7 +458,9 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float pv = __expf(s[kb][r] * a.scale + sBias[kb * 16 + 4 * g + r] - L);
-        dp[kb][r] = pv * (dp[kb][r] - D);
+        const float mul =
+            drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + myq) * T + k0 + kb * 16 + 4 * g + r);
+        dp[kb][r] = pv * (dp[kb][r] * mul - D);
       }
     if constexpr (sizeof(TI) == 2) {
 #pragma unroll
@@ -500,7 +511,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
                                        int64_t q_off, int64_t k_off, int64_t v_off,
                                        const float* key_bias, float scale, void* out,
                                        int64_t ld_out, float* lse, mmseq_dtype dtype,
-                                       mmseq_stream stream) {
+                                       const mmseq_dropout* drop, mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   MMSEQ_REQUIRE(out && lse && ld_out >= heads * 64, "attn_fwd: bad out/lse");
@@ -509,6 +520,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
   a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
   a.o_w = out; a.ld_out = ld_out; a.lse = lse;
+  a.drop = make_drop(drop);
   dim3 grid((T + QT - 1) / QT, heads, P);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MMSEQ_BF16)
@@ -523,7 +535,8 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
                                        const float* key_bias, float scale, const void* out,
                                        int64_t ld_out, const void* dout, int64_t ld_dout,
                                        const float* lse, float* delta, void* dqkv,
-                                       int64_t ld_dqkv, mmseq_dtype dtype, mmseq_stream stream) {
+                                       int64_t ld_dqkv, mmseq_dtype dtype,
+                                       const mmseq_dropout* drop, mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   const int ve = dtype == MMSEQ_BF16 ? 8 : 4;
@@ -536,6 +549,7 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
   a.out = out; a.ld_out = ld_out; a.dout = dout; a.ld_dout = ld_dout;
   a.lse = const_cast<float*>(lse); a.delta = delta; a.dqkv = dqkv; a.ld_dqkv = ld_dqkv;
+  a.drop = make_drop(drop);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t rows = (int64_t)P * T;
   dim3 gd((unsigned)((rows + 3) / 4));

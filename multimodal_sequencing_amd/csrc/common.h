@@ -102,6 +102,38 @@ __device__ __forceinline__ float act_bwd(int act, float x) {
   }
 }
 
+// --- dropout: counter-based mask (no stored masks; fwd and bwd regenerate the same bits) ---
+struct Drop {
+  uint32_t thr;     // drop iff (hash >> 8) < thr   (thr = p * 2^24); thr == 0 -> disabled
+  uint32_t stream;
+  uint64_t seed;
+  float scale;      // 1 / (1 - p)
+};
+__host__ inline Drop make_drop(const mmseq_dropout* d) {
+  Drop r;
+  r.thr = 0; r.stream = 0; r.seed = 0; r.scale = 1.f;
+  if (d && d->p > 0.f) {
+    r.thr = (uint32_t)(d->p * 16777216.0f);
+    r.stream = d->stream;
+    r.seed = d->seed;
+    r.scale = 1.0f / (1.0f - d->p);
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t idx) {
+  uint32_t h = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x9e3779b1u) ^ (uint32_t)d.seed ^
+               (d.stream * 0x85ebca77u);
+  h *= 0xcc9e2d51u;
+  h ^= (uint32_t)(d.seed >> 32) + 0x27d4eb2fu;
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;  // fmix32
+  return h;
+}
+// multiplier for element idx: 0 (dropped) or 1/(1-p); 1 when disabled
+__device__ __forceinline__ float drop_mul(const Drop& d, uint64_t idx) {
+  if (d.thr == 0) return 1.f;
+  return (drop_hash(d, idx) >> 8) < d.thr ? 0.f : d.scale;
+}
+
 // status plumbing shared by the ABI wrappers
 mmseq_status mmseq_set_error(mmseq_status code, const char* fmt, ...);
 mmseq_status mmseq_check_launch(const char* what);

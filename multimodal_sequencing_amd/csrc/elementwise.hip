@@ -66,20 +66,18 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int rows, int cols,
     if (c < cols) ws[(int64_t)blockIdx.y * cols + c] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
   }
 }
-__global__ __launch_bounds__(256) void colsum_final_kernel(int nb, int cols, const float* __restrict__ ws,
-                                                           float* __restrict__ out, int acc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += ws[(int64_t)b * cols + c];
-  out[c] = acc ? out[c] + s : s;
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void act_kernel(int64_t n, int act, const T* __restrict__ x,
                                                   T* __restrict__ y) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     Elem<T>::st(y + i, act_fwd(act, Elem<T>::ld(x + i)));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_kernel(int64_t n, const T* __restrict__ x,
+                                                      T* __restrict__ y, Drop d) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    Elem<T>::st(y + i, Elem<T>::ld(x + i) * drop_mul(d, (uint64_t)i));
 }
 
 template <typename T>
@@ -183,8 +181,13 @@ extern "C" mmseq_status mmseq_transpose_cast(int rows, int cols, const float* sr
   return mmseq_check_launch("transpose_cast");
 }
 
+int64_t mmseq_reduce_extra(int nb, int W);
+mmseq_status mmseq_reduce_partials(int nb, int W, int split, const float* ws, float* ws2,
+                                   float* outA, float* outB, int accumulate, hipStream_t s);
+
 extern "C" int64_t mmseq_colsum_workspace(int rows, int cols) {
-  return (int64_t)((rows + CS_ROWS - 1) / CS_ROWS) * cols;
+  const int nb = (rows + CS_ROWS - 1) / CS_ROWS;
+  return (int64_t)nb * cols + mmseq_reduce_extra(nb, cols);
 }
 
 extern "C" mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t ldx, float* out,
@@ -213,9 +216,10 @@ extern "C" mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t 
                            rows, cols, (const unsigned short*)x, ldx, ws);
     }
   }
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, nb, cols, ws,
-                     out, accumulate);
-  return mmseq_check_launch("colsum");
+  mmseq_status st = mmseq_check_launch("colsum");
+  if (st) return st;
+  return mmseq_reduce_partials(nb, cols, cols, ws, ws + (int64_t)nb * cols, out, nullptr, accumulate,
+                               s);
 }
 
 extern "C" mmseq_status mmseq_act_fwd(int64_t n, int act, const void* x, void* y, mmseq_dtype dt,
@@ -230,6 +234,21 @@ extern "C" mmseq_status mmseq_act_fwd(int64_t n, int act, const void* x, void* y
     hipLaunchKernelGGL(act_kernel<unsigned short>, dim3(grid_for(n)), dim3(256), 0, s, n, act,
                        (const unsigned short*)x, (unsigned short*)y);
   return mmseq_check_launch("act_fwd");
+}
+
+extern "C" mmseq_status mmseq_dropout_apply(int64_t n, const void* x, void* y, mmseq_dtype dt,
+                                            const mmseq_dropout* drop, mmseq_stream stream) {
+  MMSEQ_REQUIRE(n >= 0 && x && y, "dropout: bad args");
+  if (!n) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const Drop d = make_drop(drop);
+  if (dt == MMSEQ_F32)
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, n,
+                       (const float*)x, (float*)y, d);
+  else
+    hipLaunchKernelGGL(dropout_kernel<unsigned short>, dim3(grid_for(n)), dim3(256), 0, s, n,
+                       (const unsigned short*)x, (unsigned short*)y, d);
+  return mmseq_check_launch("dropout_apply");
 }
 
 extern "C" mmseq_status mmseq_act_bwd(int64_t n, int act, const void* z, const void* dy, void* dz,

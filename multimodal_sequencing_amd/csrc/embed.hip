@@ -7,6 +7,7 @@
 
 mmseq_status ln_reduce_partials(int nb, int cols, const float* ws, float* dg, float* db,
                                 hipStream_t s);
+int64_t mmseq_reduce_extra(int nb, int W);
 
 namespace {
 
@@ -27,7 +28,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(int P, int Lt, int H,
                                                         const float* __restrict__ beta, float eps,
                                                         T* __restrict__ joint, int64_t ld_pair,
                                                         float* __restrict__ mean,
-                                                        float* __restrict__ rstd) {
+                                                        float* __restrict__ rstd, Drop dr) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= (int64_t)P * Lt) return;
@@ -55,7 +56,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(int P, int Lt, int H,
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
     int c = j * 64 + lane;
-    if (c < H) Elem<T>::st(out + c, (v[j] - mu) * rs * gamma[c] + beta[c]);
+    if (c < H)
+      Elem<T>::st(out + c, ((v[j] - mu) * rs * gamma[c] + beta[c]) * drop_mul(dr, (uint64_t)r * H + c));
   }
   if (lane == 0) {
     mean[r] = mu;
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
                                                         int64_t ld_pair, float* __restrict__ dword,
                                                         float* __restrict__ dtype_tab,
                                                         float* __restrict__ ws_de,
-                                                        float* __restrict__ ws_ln) {
+                                                        float* __restrict__ ws_ln, Drop dr) {
   __shared__ float red[4][2][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t rows = (int64_t)P * Lt;
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
       int c = j * 64 + lane;
       if (c < H) {
         float xv = (wr[c] + pr[c] + tr[c] - mu) * rs;
-        float d = Elem<T>::ld(dyr + c);
+        float d = Elem<T>::ld(dyr + c) * drop_mul(dr, (uint64_t)r * H + c);
         xh[j] = xv;
         gdy[j] = d * gamma[c];
         pg[j] += d * xv;
@@ -349,7 +351,8 @@ extern "C" mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* 
                                            const float* type, const float* gamma,
                                            const float* beta, float eps, void* joint,
                                            int64_t ld_pair, float* mean, float* rstd,
-                                           mmseq_dtype dtype, mmseq_stream stream) {
+                                           mmseq_dtype dtype, const mmseq_dropout* drop,
+                                           mmseq_stream stream) {
   MMSEQ_REQUIRE(P >= 0 && Lt > 0 && H > 0 && H <= 1024, "embed: bad sizes");
   MMSEQ_REQUIRE(ids && word && pos && type && gamma && beta && joint && mean && rstd,
                 "embed: null buffer");
@@ -358,17 +361,19 @@ extern "C" mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* 
   dim3 grid((unsigned)(((int64_t)P * Lt + 3) / 4));
   if (dtype == MMSEQ_F32)
     hipLaunchKernelGGL(embed_fwd_kernel<float>, grid, dim3(256), 0, s, P, Lt, H, ids, tt, word,
-                       pos, type, gamma, beta, eps, (float*)joint, ld_pair, mean, rstd);
+                       pos, type, gamma, beta, eps, (float*)joint, ld_pair, mean, rstd,
+                       make_drop(drop));
   else
     hipLaunchKernelGGL(embed_fwd_kernel<unsigned short>, grid, dim3(256), 0, s, P, Lt, H, ids, tt,
                        word, pos, type, gamma, beta, eps, (unsigned short*)joint, ld_pair, mean,
-                       rstd);
+                       rstd, make_drop(drop));
   return mmseq_check_launch("embed_ln_fwd");
 }
 
 extern "C" int64_t mmseq_embed_ln_bwd_workspace(int P, int Lt, int H) {
   const int64_t rows = (int64_t)P * Lt;
-  return rows * H + ((rows + RPB - 1) / RPB) * 2 * H;
+  const int nb = (int)((rows + RPB - 1) / RPB);
+  return rows * H + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H);
 }
 
 extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* ids,
@@ -378,7 +383,7 @@ extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* 
                                            const void* djoint, int64_t ld_pair, float* dword,
                                            float* dpos, float* dtype_tab, float* dgamma,
                                            float* dbeta, float* workspace, mmseq_dtype dtype,
-                                           mmseq_stream stream) {
+                                           const mmseq_dropout* drop, mmseq_stream stream) {
   MMSEQ_REQUIRE(P >= 0 && Lt > 0 && H > 0 && H <= 1024, "embed_bwd: bad sizes");
   MMSEQ_REQUIRE(workspace && djoint && dword && dpos, "embed_bwd: null buffer");
   if (P == 0) return MMSEQ_OK;
@@ -390,11 +395,11 @@ extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* 
   if (dtype == MMSEQ_F32)
     hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, P, Lt, H, ids, tt,
                        word, pos, type, gamma, mean, rstd, (const float*)djoint, ld_pair, dword,
-                       dtype_tab, ws_de, ws_ln);
+                       dtype_tab, ws_de, ws_ln, make_drop(drop));
   else
     hipLaunchKernelGGL(embed_bwd_kernel<unsigned short>, dim3(nb), dim3(256), 0, s, P, Lt, H, ids,
                        tt, word, pos, type, gamma, mean, rstd, (const unsigned short*)djoint,
-                       ld_pair, dword, dtype_tab, ws_de, ws_ln);
+                       ld_pair, dword, dtype_tab, ws_de, ws_ln, make_drop(drop));
   hipLaunchKernelGGL(embed_pos_kernel, dim3((H + 255) / 256, Lt), dim3(256), 0, s, P, Lt, H,
                      ws_de, dpos);
   mmseq_status st = mmseq_check_launch("embed_ln_bwd");
@@ -445,7 +450,8 @@ extern "C" mmseq_status mmseq_vit_embed_fwd(int P, int ntok, int W, int npatch_i
 
 extern "C" int64_t mmseq_vit_embed_bwd_workspace(int P, int ntok, int W) {
   const int64_t rows = (int64_t)P * ntok;
-  return (int64_t)P * W + ((rows + RPB - 1) / RPB) * 2 * W;
+  const int nb = (int)((rows + RPB - 1) / RPB);
+  return (int64_t)P * W + (int64_t)nb * 2 * W + mmseq_reduce_extra(nb, 2 * W);
 }
 
 extern "C" mmseq_status mmseq_vit_embed_bwd(int P, int ntok, int W, int npatch_img,

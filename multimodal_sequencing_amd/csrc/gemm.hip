@@ -20,6 +20,8 @@
 static int g_disable_fast = 0;  // test hook: force the generic kernel
 // caller-provided split-K slab workspace (mmseq_gemm_set_workspace); stream-ordered use only
 static float* g_slab = nullptr;
+static int g_ring = 0;  // 1: BK=32 four-slot ring kernel, 0: BK=64 double-buffer kernel
+static int g_big = 1;   // 256 x 256 NT kernel: 1 for large problems, 2 always (tests)
 static int64_t g_slab_bytes = 0;
 
 namespace {
@@ -46,6 +48,7 @@ struct GemmArgs {
   const float* bias; int act; void* aux; const void* dact; const void* resid; int64_t ldr, sR;
   float alpha; int accumulate; int vec_ok; int vec_c;
   int splitk; int kchunk; float* slab;  // split-K (TN wgrad): partial slabs [splitk][M][N] f32
+  Drop drop;                            // dropout after the activation, before the residual
 };
 
 template <typename TI, bool TRANS>
@@ -136,7 +139,8 @@ __device__ __forceinline__ bf16x8_t frag_tn_bf16(const unsigned short* s, int rb
 
 template <typename TO>
 __device__ __forceinline__ void epilogue4(const GemmArgs& a, TO* __restrict__ C, const TO* resid,
-                                          TO* aux, const TO* dact, int m, int n, const float* acc) {
+                                          TO* aux, const TO* dact, int m, int n, const float* acc,
+                                          int b = 0) {
   if (m >= a.M || n >= a.N) return;
   float v[4];
   bool full = (n + 3 < a.N);
@@ -160,6 +164,11 @@ __device__ __forceinline__ void epilogue4(const GemmArgs& a, TO* __restrict__ C,
         v[r] = act_fwd(a.act, v[r]);
       }
     }
+  }
+  if (a.drop.thr) {
+    const int64_t di = ((int64_t)b * a.M + m) * a.N + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= drop_mul(a.drop, di + r);
   }
   if (resid) {
     const TO* rp = resid + (int64_t)m * a.ldr + n;
@@ -297,7 +306,7 @@ __global__ __launch_bounds__(NT_THREADS) void gemm_kernel(GemmArgs a) {
       int m = m0 + wr * 64 + i * 16 + ii;
       int n = n0 + wc * 64 + j * 16 + 4 * g;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epilogue4<TO>(a, C, resid, aux, dact, m, n, v);
+      epilogue4<TO>(a, C, resid, aux, dact, m, n, v, b);
     }
 }
 
@@ -474,7 +483,250 @@ __global__ __launch_bounds__(256, 2) void gemm_fast_kernel(GemmArgs a, int tiles
       int m = m0 + wr * 64 + i * 16 + ii;
       int n = n0 + wc * 64 + j * 16 + 4 * g;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epilogue4<TO>(a, C, resid, aux, dact, m, n, v);
+      epilogue4<TO>(a, C, resid, aux, dact, m, n, v, b);
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Ring variant: BK = 32, four-slot LDS ring (16 KB per slot), three K-steps in flight behind a
+// COUNTED vmcnt and a raw s_barrier (guide §5 "Pipelining across barriers": __syncthreads()
+// would drain every LDS-DMA with vmcnt(0)). 64 KB per workgroup -> 2 workgroups per CU.
+//   NT image: [128 rows][32 k], 64-B rows, chunk' = chunk ^ (((row >> 3) & 1) << 1)
+//   TN image: [32 k][128 m], 256-B rows, chunk' = chunk ^ ((row & 7) << 1)
+// ---------------------------------------------------------------------------------------------
+template <bool TRANS>
+__device__ __forceinline__ void stage32(rsrc_t r, int64_t ld, int k0, unsigned short* s, int wave,
+                                        int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = wave * 2 + i;
+    uint32_t voff;
+    if (!TRANS) {
+      const int row = inst * 16 + (lane >> 2), cp = lane & 3;
+      const int c = cp ^ (((row >> 3) & 1) << 1);
+      voff = (uint32_t)(((int64_t)row * ld + k0 + c * 8) * 2);
+    } else {
+      const int row = inst * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ ((row & 7) << 1);
+      voff = (uint32_t)(((int64_t)row * ld + c * 8) * 2);
+    }
+    dma16(r, s + inst * 512, voff);
+  }
+}
+
+template <bool TRANS>
+__device__ __forceinline__ bf16x8_t frag32(const unsigned short* s, int rb, int lane) {
+  if (!TRANS) {
+    const int rr = rb + (lane & 15), c = lane >> 4;
+    const unsigned short* p = s + rr * 32 + ((c ^ (((rr >> 3) & 1) << 1)) << 3);
+    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(p));
+  }
+  return frag_swz<true>(s, rb, 0, lane);
+}
+
+template <typename TO, bool TRANS>
+__global__ __launch_bounds__(256, 2) void gemm_ring_kernel(GemmArgs a, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[4 * 2 * 128 * 32];  // 64 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nwg = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int Lr = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int tm = Lr / tiles_n, tn = Lr % tiles_n;
+  const int m0 = tm * 128, n0 = tn * 128;
+  const int split = a.splitk > 1 ? blockIdx.y : 0;
+  const int b = a.splitk > 1 ? 0 : blockIdx.y;
+  const int kbeg = split * a.kchunk;
+  const int Kend = a.splitk > 1 ? min(a.K, kbeg + a.kchunk) : a.K;
+  const unsigned short* A = reinterpret_cast<const unsigned short*>(a.A) + (int64_t)b * a.sA;
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(a.B) + (int64_t)b * a.sB;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (Kend - kbeg + 31) / 32;
+  rsrc_t ra, rb;
+  if (!TRANS) {
+    ra = make_rsrc(A + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
+    rb = make_rsrc(B + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
+  }
+  auto issue = [&](int kt) {
+    unsigned short* sA = smem + (kt & 3) * 8192;
+    unsigned short* sB = sA + 4096;
+    const int k0 = kbeg + kt * 32;
+    if (!TRANS) {
+      stage32<false>(ra, a.lda, k0, sA, wave, lane);
+      stage32<false>(rb, a.ldb, k0, sB, wave, lane);
+    } else {
+      rsrc_t ta = make_rsrc(A + (int64_t)k0 * a.lda + m0,
+                            ((int64_t)(Kend - k0 - 1) * a.lda + (a.M - m0)) * 2);
+      rsrc_t tb = make_rsrc(B + (int64_t)k0 * a.ldb + n0,
+                            ((int64_t)(Kend - k0 - 1) * a.ldb + (a.N - n0)) * 2);
+      stage32<true>(ta, a.lda, k0, sA, wave, lane);
+      stage32<true>(tb, a.ldb, k0, sB, wave, lane);
+    }
+  };
+
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire this wave's DMA for step kt; later steps (4 instructions each) may stay in flight
+    const int later = nk - 1 - kt;
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for kt landed; slot (kt-1)&3 fully read
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 3 < nk) issue(kt + 3);
+    const unsigned short* sA = smem + (kt & 3) * 8192;
+    const unsigned short* sB = sA + 4096;
+    bf16x8_t fa[4], fb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i] = frag32<TRANS>(sA, wr * 64 + i * 16, lane);
+      fb[i] = frag32<TRANS>(sB, wc * 64 + i * 16, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  }
+
+  const int g = lane >> 4, ii = lane & 15;
+  if (a.splitk > 1) {
+    float* slab = a.slab + (int64_t)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int m = m0 + wr * 64 + i * 16 + ii;
+        int n = n0 + wc * 64 + j * 16 + 4 * g;
+        if (m < a.M && n < a.N)
+          *reinterpret_cast<f32x4*>(slab + (int64_t)m * a.N + n) = acc[i][j];
+      }
+    return;
+  }
+  TO* C = reinterpret_cast<TO*>(a.C) + (int64_t)b * a.sC;
+  const TO* resid = a.resid ? reinterpret_cast<const TO*>(a.resid) + (int64_t)b * a.sR : nullptr;
+  TO* aux = a.aux ? reinterpret_cast<TO*>(a.aux) + (int64_t)b * a.sC : nullptr;
+  const TO* dact = a.dact ? reinterpret_cast<const TO*>(a.dact) + (int64_t)b * a.sC : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m = m0 + wr * 64 + i * 16 + ii;
+      int n = n0 + wc * 64 + j * 16 + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epilogue4<TO>(a, C, resid, aux, dact, m, n, v, b);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large NT kernel (forward / dgrad over the 164k-row activations): 256 x 256 output tile,
+// 8 waves (2 along M x 4 along N, 128 x 64 each = 8 x 4 MFMA 16x16 tiles), BK = 64, one block
+// per CU. Per K-step the block reads 64 KB of operands into LDS and every wave reads 24 KB of
+// fragments (A 16 KB + B 8 KB): 1536 LDS cycles against 2048 MFMA cycles per SIMD pair, where
+// the 128 x 128 tile needs 100 % of the LDS port (the ~900 TF ceiling of guide §5).
+// Pipeline: two 64 KB buffers, K-tile t + 2 is staged (LDS-DMA, swizzled images as in the
+// 128 x 128 NT path) as soon as every wave has read K-tile t's fragments; the wait for a K-tile
+// is a COUNTED vmcnt (the next K-tile's 8 DMAs per lane stay in flight) and raw s_barriers.
+// ---------------------------------------------------------------------------------------------
+template <typename TO>
+__global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 4 * 8192];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nwg = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int Lr = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int tm = Lr / tiles_n, tn = Lr % tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int b = blockIdx.y;
+  const unsigned short* A = reinterpret_cast<const unsigned short*>(a.A) + (int64_t)b * a.sA;
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(a.B) + (int64_t)b * a.sB;
+  const rsrc_t ra = make_rsrc(A + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
+  const rsrc_t rb = make_rsrc(B + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // half-tiles: 0 = A rows 0..127, 1 = A rows 128..255, 2/3 = B likewise; 2 DMAs per lane each
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      unsigned short* sh = smem + (buf * 4 + h) * 8192;
+      const int64_t ld = h < 2 ? a.lda : a.ldb;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int inst = wave * 2 + i;
+        const int row = inst * 8 + (lane >> 3), cp = lane & 7;
+        const int c = cp ^ ((row >> 1) & 7);
+        const uint32_t voff = (uint32_t)((((int64_t)((h & 1) * 128 + row)) * ld + k0 + c * 8) * 2);
+        dma16(h < 2 ? ra : rb, sh + inst * 512, voff);
+      }
+    }
+  };
+
+  const int nk = a.K / 64;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // K-tile t landed for every wave
+    asm volatile("" ::: "memory");
+    const unsigned short* sA = smem + ((t & 1) * 4 + wr) * 8192;
+    const unsigned short* sB = smem + ((t & 1) * 4 + 2 + (wc >> 1)) * 8192;
+    bf16x8_t fa[2][8], fb[2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[ks][j] = frag_swz<false>(sB, (wc & 1) * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[ks][i] = frag_swz<false>(sA, i * 16, ks, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j], fa[0][i], acc[i][j], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave holds K-tile t in registers: buffer t & 1 free
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) issue(t + 2, t & 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j], fa[1][i], acc[i][j], 0, 0, 0);
+  }
+
+  const int g = lane >> 4, ii = lane & 15;
+  TO* C = reinterpret_cast<TO*>(a.C) + (int64_t)b * a.sC;
+  const TO* resid = a.resid ? reinterpret_cast<const TO*>(a.resid) + (int64_t)b * a.sR : nullptr;
+  TO* aux = a.aux ? reinterpret_cast<TO*>(a.aux) + (int64_t)b * a.sC : nullptr;
+  const TO* dact = a.dact ? reinterpret_cast<const TO*>(a.dact) + (int64_t)b * a.sC : nullptr;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m = m0 + wr * 128 + i * 16 + ii;
+      int n = n0 + wc * 64 + j * 16 + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epilogue4<TO>(a, C, resid, aux, dact, m, n, v, b);
     }
 }
 
@@ -496,8 +748,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 
 template <typename TO>
 hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s) {
+  if (!trans && g_big && a.splitk == 1 &&
+      (g_big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) * batch >= 512)) {
+    const int tn = (a.N + 255) / 256;
+    dim3 grid(((a.M + 255) / 256) * tn, batch);
+    hipLaunchKernelGGL((gemm256_nt_kernel<TO>), grid, dim3(512), 0, s, a, tn);
+    return hipGetLastError();
+  }
   const int tiles_m = (a.M + 127) / 128, tiles_n = (a.N + 127) / 128;
   dim3 grid(tiles_m * tiles_n, a.splitk > 1 ? a.splitk : batch);
+  if (g_ring) {
+    if (trans)
+      hipLaunchKernelGGL((gemm_ring_kernel<TO, true>), grid, dim3(256), 0, s, a, tiles_n);
+    else
+      hipLaunchKernelGGL((gemm_ring_kernel<TO, false>), grid, dim3(256), 0, s, a, tiles_n);
+    return hipGetLastError();
+  }
   if (trans)
     hipLaunchKernelGGL((gemm_fast_kernel<TO, true>), grid, dim3(256), 0, s, a, tiles_n);
   else
@@ -509,7 +775,13 @@ inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 }  // namespace
 
-extern "C" void mmseq_gemm_set_fast(int enable) { g_disable_fast = !enable; }
+extern "C" void mmseq_gemm_set_fast(int enable) {
+  // 1 = default (256^2 NT for large problems, double-buffer 128^2 otherwise), 2 = double-buffer
+  // 128^2 only, 3 = ring 128^2 only, 4 = 256^2 NT whenever its preconditions hold, 0 = generic
+  g_disable_fast = enable == 0;
+  g_big = enable == 1 ? 1 : (enable == 4 ? 2 : 0);
+  g_ring = enable == 3;
+}
 
 extern "C" void mmseq_gemm_set_workspace(void* ws, int64_t bytes) {
   g_slab = reinterpret_cast<float*>(ws);
@@ -522,7 +794,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
                                    const float* bias, int act, void* aux_out, const void* dact_aux,
                                    const void* resid, int64_t ldr, int64_t strideR, float alpha,
                                    int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
-                                   mmseq_stream stream) {
+                                   const mmseq_dropout* drop, mmseq_stream stream) {
   MMSEQ_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes M=%d N=%d K=%d b=%d",
                 M, N, K, batch);
   MMSEQ_REQUIRE(A && B && C, "gemm: null operand");
@@ -544,6 +816,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   a.bias = bias; a.act = act; a.aux = aux_out; a.dact = dact_aux;
   a.resid = resid; a.ldr = resid ? ldr : 0; a.sR = strideR;
   a.alpha = alpha; a.accumulate = accumulate;
+  a.drop = make_drop(drop);
   const int ve = in_dtype == MMSEQ_BF16 ? 8 : 4;
   a.vec_ok = al16(A) && al16(B) && lda % ve == 0 && ldb % ve == 0 && strideA % ve == 0 &&
              strideB % ve == 0;
@@ -559,6 +832,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   if (fast_ok) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     const bool plain = !bias && !act && !aux_out && !dact_aux && !resid && alpha == 1.0f &&
+                       !a.drop.thr &&
                        out_dtype == MMSEQ_F32 && batch == 1 && ldc % 4 == 0 && al16(C);
     int S = 1;
     if (trans && plain && g_slab && tiles < 512) {

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void span_fwd_kernel(int P, int Lt, int H, con
                                                        int64_t ld_pair, const float* __restrict__ score,
                                                        const int64_t* __restrict__ sep,
                                                        float* __restrict__ probs,
-                                                       float* __restrict__ mix) {
+                                                       float* __restrict__ mix, Drop drop) {
   __shared__ float pr[2][MAXLT];
   __shared__ float red[4];
   const int p = blockIdx.x;
@@ -154,6 +154,7 @@ __global__ __launch_bounds__(256) void span_fwd_kernel(int P, int Lt, int H, con
     for (int t = threadIdx.x; t < Lt; t += 256) {
       pr[s][t] *= inv;
       probs[((int64_t)p * 2 + s) * Lt + t] = pr[s][t];
+      pr[s][t] *= drop_mul(drop, ((uint64_t)p * 2 + s) * Lt + t);  // :735 (after softmax)
     }
   }
   __syncthreads();
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) void span_bwd_kernel(int P, int Lt, int H, con
                                                        const int64_t* __restrict__ sep,
                                                        const float* __restrict__ dmix,
                                                        float* __restrict__ dscore,
-                                                       T* __restrict__ dtop) {
+                                                       T* __restrict__ dtop, Drop drop) {
   __shared__ float dpr[2][MAXLT];
   __shared__ float red[4];
   const int p = blockIdx.x;
@@ -194,9 +195,9 @@ __global__ __launch_bounds__(256) void span_bwd_kernel(int P, int Lt, int H, con
     }
     a0 = wave_sum(a0);
     a1 = wave_sum(a1);
-    if (lane == 0) {
-      dpr[0][t] = a0;
-      dpr[1][t] = a1;
+    if (lane == 0) {  // gradient w.r.t. the undropped probabilities
+      dpr[0][t] = a0 * drop_mul(drop, ((uint64_t)p * 2 + 0) * Lt + t);
+      dpr[1][t] = a1 * drop_mul(drop, ((uint64_t)p * 2 + 1) * Lt + t);
     }
   }
   __syncthreads();
@@ -217,7 +218,8 @@ __global__ __launch_bounds__(256) void span_bwd_kernel(int P, int Lt, int H, con
   }
   T* dtp = dtop + (int64_t)p * ld_pair;
   for (int t = 0; t < Lt; ++t) {
-    const float w0 = pr0[t], w1 = pr1[t];
+    const float w0 = pr0[t] * drop_mul(drop, ((uint64_t)p * 2 + 0) * Lt + t);
+    const float w1 = pr1[t] * drop_mul(drop, ((uint64_t)p * 2 + 1) * Lt + t);
     for (int h = threadIdx.x; h < H; h += 256) {
       T* d = dtp + (int64_t)t * H + h;
       Elem<T>::st(d, Elem<T>::ld(d) + w0 * dm0[h] + w1 * dm1[h]);
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(256) void small_attn_fwd_kernel(int B, int T, int h
                                                              const float* __restrict__ v,
                                                              const float* __restrict__ kbias,
                                                              float scale, float* __restrict__ out,
-                                                             float* __restrict__ probs) {
+                                                             float* __restrict__ probs, Drop drop) {
   __shared__ float S[SA_T][SA_T + 1];
   const int b = blockIdx.x / heads, h = blockIdx.x % heads;
   const int D = heads * d;
@@ -263,7 +265,9 @@ __global__ __launch_bounds__(256) void small_attn_fwd_kernel(int B, int T, int h
     float inv = 1.f / sum;
     for (int j = 0; j < T; ++j) {
       S[i][j] *= inv;
-      probs[(((int64_t)b * heads + h) * T + i) * T + j] = S[i][j];
+      const uint64_t idx = (((uint64_t)b * heads + h) * T + i) * T + j;
+      probs[idx] = S[i][j];
+      S[i][j] *= drop_mul(drop, idx);  // neural.py:228
     }
   }
   __syncthreads();
@@ -283,18 +287,22 @@ __global__ __launch_bounds__(256) void small_attn_bwd_kernel(int B, int T, int h
                                                              const float* __restrict__ dout,
                                                              float scale, float* __restrict__ dq,
                                                              float* __restrict__ dk,
-                                                             float* __restrict__ dv) {
+                                                             float* __restrict__ dv, Drop drop) {
   __shared__ float Pm[SA_T][SA_T + 1];
+  __shared__ float Mk[SA_T][SA_T + 1];  // dropout multipliers
   __shared__ float dS[SA_T][SA_T + 1];
   const int b = blockIdx.x / heads, h = blockIdx.x % heads;
   const int D = heads * d;
   const int64_t off = (int64_t)b * T * D + h * d;
   for (int e = threadIdx.x; e < T * T; e += 256) {
     int i = e / T, j = e % T;
-    Pm[i][j] = probs[(((int64_t)b * heads + h) * T + i) * T + j];
+    const uint64_t idx = (((uint64_t)b * heads + h) * T + i) * T + j;
+    Pm[i][j] = probs[idx];
+    const float mk = drop_mul(drop, idx);
+    Mk[i][j] = mk;
     float s = 0.f;
     for (int c = 0; c < d; ++c) s += dout[off + (int64_t)i * D + c] * v[off + (int64_t)j * D + c];
-    dS[i][j] = s;  // dP
+    dS[i][j] = s * mk;  // dP w.r.t. the undropped probabilities
   }
   __syncthreads();
   for (int i = threadIdx.x; i < T; i += 256) {
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(256) void small_attn_bwd_kernel(int B, int T, int h
     for (int j = 0; j < T; ++j) {
       aq += dS[i][j] * k[off + (int64_t)j * D + c];
       ak += dS[j][i] * q[off + (int64_t)j * D + c];
-      av += Pm[j][i] * dout[off + (int64_t)j * D + c];
+      av += Pm[j][i] * Mk[j][i] * dout[off + (int64_t)j * D + c];
     }
     dq[off + (int64_t)i * D + c] = aq * scale;
     dk[off + (int64_t)i * D + c] = ak * scale;
@@ -353,61 +361,67 @@ extern "C" mmseq_status mmseq_pointer_bwd(int B, int N, int H, const float* q, c
 extern "C" mmseq_status mmseq_span_pool_fwd(int P, int Lt, int H, const void* top,
                                             int64_t ld_pair, const float* score,
                                             const int64_t* sep, float* probs, float* mix,
-                                            mmseq_dtype dt, mmseq_stream stream) {
+                                            mmseq_dtype dt, const mmseq_dropout* drop,
+                                            mmseq_stream stream) {
   MMSEQ_REQUIRE(P >= 0 && Lt > 0 && Lt <= MAXLT && H > 0, "span_pool: Lt must be <= %d", MAXLT);
   MMSEQ_REQUIRE(top && score && sep && probs && mix, "span_pool_fwd: null buffer");
   if (!P) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dt == MMSEQ_F32)
     hipLaunchKernelGGL(span_fwd_kernel<float>, dim3(P), dim3(256), 0, s, P, Lt, H,
-                       (const float*)top, ld_pair, score, sep, probs, mix);
+                       (const float*)top, ld_pair, score, sep, probs, mix, make_drop(drop));
   else
     hipLaunchKernelGGL(span_fwd_kernel<unsigned short>, dim3(P), dim3(256), 0, s, P, Lt, H,
-                       (const unsigned short*)top, ld_pair, score, sep, probs, mix);
+                       (const unsigned short*)top, ld_pair, score, sep, probs, mix,
+                       make_drop(drop));
   return mmseq_check_launch("span_pool_fwd");
 }
 
 extern "C" mmseq_status mmseq_span_pool_bwd(int P, int Lt, int H, const void* top,
                                             int64_t ld_pair, const float* probs,
                                             const int64_t* sep, const float* dmix, float* dscore,
-                                            void* dtop, mmseq_dtype dt, mmseq_stream stream) {
+                                            void* dtop, mmseq_dtype dt, const mmseq_dropout* drop,
+                                            mmseq_stream stream) {
   MMSEQ_REQUIRE(P >= 0 && Lt > 0 && Lt <= MAXLT && H > 0, "span_pool_bwd: bad sizes");
   MMSEQ_REQUIRE(top && probs && sep && dmix && dscore && dtop, "span_pool_bwd: null buffer");
   if (!P) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dt == MMSEQ_F32)
     hipLaunchKernelGGL(span_bwd_kernel<float>, dim3(P), dim3(256), 0, s, P, Lt, H,
-                       (const float*)top, ld_pair, probs, sep, dmix, dscore, (float*)dtop);
+                       (const float*)top, ld_pair, probs, sep, dmix, dscore, (float*)dtop,
+                       make_drop(drop));
   else
     hipLaunchKernelGGL(span_bwd_kernel<unsigned short>, dim3(P), dim3(256), 0, s, P, Lt, H,
                        (const unsigned short*)top, ld_pair, probs, sep, dmix, dscore,
-                       (unsigned short*)dtop);
+                       (unsigned short*)dtop, make_drop(drop));
   return mmseq_check_launch("span_pool_bwd");
 }
 
 extern "C" mmseq_status mmseq_small_attn_fwd(int B, int T, int heads, int d, const float* q,
                                              const float* k, const float* v,
                                              const float* key_bias, float scale, float* out,
-                                             float* probs, mmseq_stream stream) {
+                                             float* probs, const mmseq_dropout* drop,
+                                             mmseq_stream stream) {
   MMSEQ_REQUIRE(B >= 0 && T > 0 && T <= SA_T && heads > 0 && d > 0, "small_attn: T must be <= %d",
                 SA_T);
   MMSEQ_REQUIRE(q && k && v && out && probs, "small_attn_fwd: null buffer");
   if (!B) return MMSEQ_OK;
   hipLaunchKernelGGL(small_attn_fwd_kernel, dim3(B * heads), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), B, T, heads, d, q, k, v, key_bias,
-                     scale, out, probs);
+                     scale, out, probs, make_drop(drop));
   return mmseq_check_launch("small_attn_fwd");
 }
 
 extern "C" mmseq_status mmseq_small_attn_bwd(int B, int T, int heads, int d, const float* q,
                                              const float* k, const float* v, const float* probs,
                                              const float* dout, float scale, float* dq, float* dk,
-                                             float* dv, mmseq_stream stream) {
+                                             float* dv, const mmseq_dropout* drop,
+                                             mmseq_stream stream) {
   MMSEQ_REQUIRE(B >= 0 && T > 0 && T <= SA_T && heads > 0 && d > 0, "small_attn_bwd: bad sizes");
   MMSEQ_REQUIRE(q && k && v && probs && dout && dq && dk && dv, "small_attn_bwd: null buffer");
   if (!B) return MMSEQ_OK;
   hipLaunchKernelGGL(small_attn_bwd_kernel, dim3(B * heads), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), B, T, heads, d, q, k, v, probs, dout,
-                     scale, dq, dk, dv);
+                     scale, dq, dk, dv, make_drop(drop));
   return mmseq_check_launch("small_attn_bwd");
 }

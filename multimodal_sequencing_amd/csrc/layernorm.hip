@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
                                                      const float* __restrict__ beta, float eps,
                                                      TY* __restrict__ y, mmseq_rows yl,
                                                      float* __restrict__ mean,
-                                                     float* __restrict__ rstd) {
+                                                     float* __restrict__ rstd, Drop dy_) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
     if (c >= cols) continue;
     f32x4 g = ldp(gamma, c, cols), b = ldp(beta, c, cols), o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * g[e] + b[e];
+    for (int e = 0; e < 4; ++e)
+      o[e] = ((v[j][e] - mu) * rs * g[e] + b[e]) * drop_mul(dy_, (uint64_t)r * cols + c + e);
     st4<TY, VEC>(yr, c, cols, o);
   }
   if (lane == 0) {
@@ -98,7 +99,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
                                                      const float* __restrict__ gamma,
                                                      T* __restrict__ dx, mmseq_rows dxl,
                                                      const T* __restrict__ dres, mmseq_rows dresl,
-                                                     float* __restrict__ ws) {
+                                                     float* __restrict__ ws, Drop din,
+                                                     T* __restrict__ dxd, Drop dout) {
   __shared__ float red[4][2][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4 pg[MAXJ], pb[MAXJ], gm[MAXJ];
@@ -118,6 +120,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
     for (int j = 0; j < MAXJ; ++j) {
       const int c = j * 256 + lane * 4;
       f32x4 xv = ld4<T, VEC>(xr, c, cols), d = ld4<T, VEC>(dyr, c, cols);
+      if (din.thr) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] *= drop_mul(din, (uint64_t)r * cols + c + e);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool in = c + e < cols;
@@ -141,6 +147,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = rs * (gdy[j][e] - s1 - xh[j][e] * s2);
+      if (dxd) {
+        f32x4 od;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) od[e] = o[e] * drop_mul(dout, (uint64_t)r * cols + c + e);
+        st4<T, VEC>(dxd + row_off(dxl, r), c, cols, od);
+      }
       if (drr) {
         f32x4 dr = ld4<T, VEC>(drr, c, cols);
 #pragma unroll
@@ -168,43 +180,28 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
   }
 }
 
-// sum ws[nb][2][cols] over nb in a fixed order -> dgamma, dbeta (+=)
-__global__ __launch_bounds__(256) void ln_reduce_kernel(int nb, int cols, const float* __restrict__ ws,
-                                                        float* __restrict__ dg,
-                                                        float* __restrict__ db) {
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int idx = blockIdx.x * 64 + lane;  // 0 .. 2*cols-1
-  const int which = idx / cols, c = idx % cols;
-  float s = 0.f;
-  if (idx < 2 * cols)
-    for (int b = wave; b < nb; b += 4) s += ws[((int64_t)b * 2 + which) * cols + c];
-  part[wave][lane] = s;
-  __syncthreads();
-  if (wave == 0 && idx < 2 * cols) {
-    float t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-    float* dst = which == 0 ? dg : db;
-    if (dst) dst[c] += t;
-  }
-}
-
 bool rows_vec(const void* p, const mmseq_rows& l, int esz) {
   return ((uintptr_t)p % (4 * esz)) == 0 && l.ld % 4 == 0 && l.bstride % 4 == 0;
 }
 
 }  // namespace
 
+int64_t mmseq_reduce_extra(int nb, int W);
+mmseq_status mmseq_reduce_partials(int nb, int W, int split, const float* ws, float* ws2,
+                                   float* outA, float* outB, int accumulate, hipStream_t s);
+
+// ws must hold nb*2*cols partials followed by mmseq_reduce_extra(nb, 2*cols) scratch floats
 mmseq_status ln_reduce_partials(int nb, int cols, const float* ws, float* dg, float* db,
                                 hipStream_t s) {
-  hipLaunchKernelGGL(ln_reduce_kernel, dim3((2 * cols + 63) / 64), dim3(256), 0, s, nb, cols, ws,
-                     dg, db);
-  return mmseq_check_launch("ln_reduce");
+  return mmseq_reduce_partials(nb, 2 * cols, cols, ws, const_cast<float*>(ws) + (int64_t)nb * 2 * cols,
+                               dg, db, 1, s);
 }
 
 extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, mmseq_rows xl,
                                             const float* gamma, const float* beta, float eps,
                                             void* y, mmseq_rows yl, float* mean, float* rstd,
-                                            mmseq_dtype xd, mmseq_dtype yd, mmseq_stream stream) {
+                                            mmseq_dtype xd, mmseq_dtype yd,
+                                            const mmseq_dropout* drop_y, mmseq_stream stream) {
   MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 1024, "layernorm: cols must be in (0, 1024]");
   MMSEQ_REQUIRE(x && y && gamma && beta, "layernorm: null buffer");
   MMSEQ_REQUIRE(xl.rpb > 0 && yl.rpb > 0, "layernorm: rpb must be > 0");
@@ -213,9 +210,10 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
   dim3 grid((rows + 3) / 4);
   const bool vec = cols % 4 == 0 && rows_vec(x, xl, xd == MMSEQ_BF16 ? 2 : 4) &&
                    rows_vec(y, yl, yd == MMSEQ_BF16 ? 2 : 4);
+  const Drop dd = make_drop(drop_y);
 #define LNF(TX, TY, V)                                                                           \
   hipLaunchKernelGGL((ln_fwd_kernel<TX, TY, V>), grid, dim3(256), 0, s, rows, cols, (const TX*)x, \
-                     xl, gamma, beta, eps, (TY*)y, yl, mean, rstd)
+                     xl, gamma, beta, eps, (TY*)y, yl, mean, rstd, dd)
 #define LNF2(TX, TY) \
   if (vec) LNF(TX, TY, true); else LNF(TX, TY, false)
   if (xd == MMSEQ_F32 && yd == MMSEQ_F32) { LNF2(float, float); }
@@ -228,7 +226,8 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
 }
 
 extern "C" int64_t mmseq_layernorm_bwd_workspace(int rows, int cols) {
-  return (int64_t)((rows + RPB - 1) / RPB) * 2 * cols;
+  const int nb = (rows + RPB - 1) / RPB;
+  return (int64_t)nb * 2 * cols + mmseq_reduce_extra(nb, 2 * cols);
 }
 
 extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
@@ -236,7 +235,9 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
                                             const float* rstd, const float* gamma, void* dx,
                                             mmseq_rows dxl, const void* dres, mmseq_rows dresl,
                                             float* dgamma, float* dbeta, float* workspace,
-                                            mmseq_dtype dtype, mmseq_stream stream) {
+                                            mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                            void* dx_drop, const mmseq_dropout* drop_dx,
+                                            mmseq_stream stream) {
   MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 1024, "layernorm_bwd: cols must be in (0, 1024]");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "layernorm_bwd: null buffer");
   if (rows == 0) return MMSEQ_OK;
@@ -245,11 +246,13 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
   const int nb = (rows + RPB - 1) / RPB;
   const int esz = dtype == MMSEQ_BF16 ? 2 : 4;
   const bool vec = cols % 4 == 0 && rows_vec(dy, dyl, esz) && rows_vec(x, xl, esz) &&
-                   rows_vec(dx, dxl, esz) && (!dres || rows_vec(dres, dresl, esz));
+                   rows_vec(dx, dxl, esz) && (!dres || rows_vec(dres, dresl, esz)) &&
+                   (!dx_drop || ((uintptr_t)dx_drop % (4 * esz)) == 0);
+  const Drop din = make_drop(drop_dy), dout = make_drop(drop_dx);
 #define LNB(T, V)                                                                                 \
   hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy,  \
                      dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl, \
-                     workspace)
+                     workspace, din, (T*)dx_drop, dout)
   if (dtype == MMSEQ_F32) {
     if (vec) LNB(float, true); else LNB(float, false);
   } else {

@@ -34,13 +34,13 @@ def _wgrad(dy, x, gW):
            accumulate=True)
 
 
-def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=None):
-    """y = act(x W^T + b) (+ resid); W [out][in] compute dtype."""
+def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=None, drop=None):
+    """y = dropout(act(x W^T + b)) (+ resid); W [out][in] compute dtype."""
     R = x.numel() // x.shape[-1]
     n_out = W.shape[0]
     if out is None:
         out = torch.empty(R, n_out, device=x.device, dtype=out_dtype or x.dtype)
-    N.gemm(x, W, out, R, n_out, x.shape[-1], bias=bias, act=act, aux=aux, resid=resid)
+    N.gemm(x, W, out, R, n_out, x.shape[-1], bias=bias, act=act, aux=aux, resid=resid, drop=drop)
     return out
 
 
@@ -52,6 +52,32 @@ def _dgrad(dy, WT, resid=None, act=0, dact=None, out=None):
         out = torch.empty(R, n_in, device=dy.device, dtype=dy.dtype)
     N.gemm(dy, WT, out, R, n_in, dy.shape[-1], resid=resid, act=act, dact=dact)
     return out
+
+
+class Dropouts:
+    """Train-mode dropout descriptors for one forward pass.
+
+    Masks are counter-based (include/mmseq.h `mmseq_dropout`): a site is identified by a 32-bit
+    stream id, a forward pass by a 64-bit seed, so the backward regenerates every mask from the
+    descriptor saved on the autograd context and nothing T x T or [rows][H] is stored.
+    `site(p, *key)` returns None in eval mode or when p == 0 (the kernels then skip the hash).
+    """
+
+    def __init__(self, seed, training):
+        self.seed = seed
+        self.training = training
+
+    def site(self, p, *key):
+        if not self.training or p <= 0:
+            return None
+        h = 0x811C9DC5
+        for k in key:  # FNV-1a over the site key -> stream id
+            for ch in str(k).encode():
+                h = ((h ^ ch) * 0x01000193) & 0xFFFFFFFF
+        return N.drop(p, h, self.seed)
+
+
+EVAL = Dropouts(0, False)
 
 
 class LayerRefs:
@@ -67,17 +93,19 @@ class LayerRefs:
 # ================================================================================================
 class BertLayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps):
+    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps, drops=(None, None, None)):
+        """drops = (attention probs :419, self-output dense :437, output dense :491)."""
         st = L.store
         H = x.shape[-1]
+        d_att, d_o, d_out = drops
         Wqkv = st.packed(L.qkv_w, "w")
         bqkv = st.packed(L.qkv_b, "f32").view(-1)
         qkv = _linear(x, Wqkv, bias=bqkv)
         o = torch.empty_like(x)
         lse = torch.empty(P, heads, T, device=x.device)
         N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
-                   H, lse)
-        s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x)
+                   H, lse, drop=d_att)
+        s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, drop=d_o)
         h1 = torch.empty_like(x)
         m1 = torch.empty(s1.shape[0], device=x.device)
         r1 = torch.empty_like(m1)
@@ -85,48 +113,56 @@ class BertLayerFn(torch.autograd.Function):
                         _rows(H), m1, r1)
         z = torch.empty(x.shape[0], st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype)
         gact = _linear(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU, aux=z)
-        s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1)
+        s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1, drop=d_out)
         y = torch.empty_like(x)
         m2 = torch.empty_like(m1)
         r2 = torch.empty_like(m1)
         N.layernorm_fwd(s2.shape[0], H, s2, _rows(H), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y,
                         _rows(H), m2, r2)
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
-        ctx.meta = (L, P, T, heads)
+        ctx.meta = (L, P, T, heads, drops)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2 = ctx.saved_tensors
-        L, P, T, heads = ctx.meta
+        L, P, T, heads, (d_att, d_o, d_out) = ctx.meta
         st = L.store
         H = x.shape[-1]
         dy = dy.contiguous()
         R = x.shape[0]
+        # LN backward also emits the dense-branch gradient through the dropout mask (ds2d) while
+        # the residual branch keeps the unmasked one (ds2)
         ds2 = torch.empty_like(dy)
+        ds2d = torch.empty_like(dy) if d_out is not None else ds2
         N.layernorm_bwd(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
-                        None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b))
-        _wgrad(ds2, gact, st.g(L.out_w))
-        _colsum(ds2, st.g(L.out_b))
-        dz = _dgrad(ds2, st.wt(L.out_w), act=GELU, dact=z)
+                        None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b),
+                        dx_drop=ds2d if d_out is not None else None, drop_dx=d_out)
+        _wgrad(ds2d, gact, st.g(L.out_w))
+        _colsum(ds2d, st.g(L.out_b))
+        dz = _dgrad(ds2d, st.wt(L.out_w), act=GELU, dact=z)
+        del ds2d
         _wgrad(dz, h1, st.g(L.i_w))
         _colsum(dz, st.g(L.i_b))
         dh1 = _dgrad(dz, st.wt(L.i_w), resid=ds2)
         del dz
         ds1 = torch.empty_like(dy)
+        ds1d = torch.empty_like(dy) if d_o is not None else ds1
         N.layernorm_bwd(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
-                        None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b))
-        _wgrad(ds1, o, st.g(L.o_w))
-        _colsum(ds1, st.g(L.o_b))
-        do = _dgrad(ds1, st.wt(L.o_w))
+                        None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
+                        dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
+        _wgrad(ds1d, o, st.g(L.o_w))
+        _colsum(ds1d, st.g(L.o_b))
+        do = _dgrad(ds1d, st.wt(L.o_w))
+        del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
         N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
-                   H, do, H, lse, delta, dqkv, 3 * H)
+                   H, do, H, lse, delta, dqkv, 3 * H, drop=d_att)
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"))
         _colsum(dqkv, st.packed(L.qkv_b, "g").view(-1))
         dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 # ================================================================================================
@@ -272,7 +308,8 @@ class VitProjFn(torch.autograd.Function):
 # ================================================================================================
 class JointInputFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, vout, ids, tt, attn_mask, anchor, L, P, Lt, Tv, eps, cdtype):
+    def forward(ctx, vout, ids, tt, attn_mask, anchor, L, P, Lt, Tv, eps, cdtype, drops=(None, None)):
+        """drops = (BertEmbeddings :369, VisualFeatEncoder :601)."""
         st = L.store
         H = st.f32(L.word).shape[1]
         T = Lt + Tv
@@ -281,25 +318,25 @@ class JointInputFn(torch.autograd.Function):
         me = torch.empty(P * Lt, device=dev)
         re = torch.empty_like(me)
         N.embed_ln_fwd(P, Lt, H, ids, tt, st.f32(L.word), st.f32(L.pos), st.f32(L.type),
-                       st.f32(L.eln_w), st.f32(L.eln_b), eps, joint, T * H, me, re)
+                       st.f32(L.eln_w), st.f32(L.eln_b), eps, joint, T * H, me, re, drop=drops[0])
         saved = [ids, tt, me, re]
         if vout is not None:
             vpre = _linear(vout, st.w(L.v_w), bias=st.f32(L.v_b))
             mv = torch.empty(P * Tv, device=dev)
             rv = torch.empty_like(mv)
             N.layernorm_fwd(P * Tv, H, vpre, _rows(H), st.f32(L.vln_w), st.f32(L.vln_b), eps,
-                            joint[Lt:], N.rows(H, T * H, Tv), mv, rv)
+                            joint[Lt:], N.rows(H, T * H, Tv), mv, rv, drop=drops[1])
             saved += [vout, vpre, mv, rv]
         key_bias = torch.zeros(P, T, device=dev)
         key_bias[:, :Lt] = (1.0 - attn_mask.float()) * -10000.0
         ctx.save_for_backward(*saved)
-        ctx.meta = (L, P, Lt, Tv, vout is not None)
+        ctx.meta = (L, P, Lt, Tv, vout is not None, drops)
         ctx.mark_non_differentiable(key_bias)
         return joint, key_bias
 
     @staticmethod
     def backward(ctx, djoint, _dkb):
-        L, P, Lt, Tv, has_v = ctx.meta
+        L, P, Lt, Tv, has_v, drops = ctx.meta
         st = L.store
         sv = ctx.saved_tensors
         ids, tt, me, re = sv[:4]
@@ -308,18 +345,18 @@ class JointInputFn(torch.autograd.Function):
         djoint = djoint.contiguous()
         N.embed_ln_bwd(P, Lt, H, ids, tt, st.f32(L.word), st.f32(L.pos), st.f32(L.type),
                        st.f32(L.eln_w), me, re, djoint, T * H, st.g(L.word), st.g(L.pos),
-                       st.g(L.type), st.g(L.eln_w), st.g(L.eln_b))
+                       st.g(L.type), st.g(L.eln_w), st.g(L.eln_b), drop=drops[0])
         dvout = None
         if has_v:
             vout, vpre, mv, rv = sv[4:]
             dvpre = torch.empty_like(vpre)
             N.layernorm_bwd(P * Tv, H, djoint[Lt:], N.rows(H, T * H, Tv), vpre, _rows(H), mv, rv,
                             st.f32(L.vln_w), dvpre, _rows(H), None, _rows(H), st.g(L.vln_w),
-                            st.g(L.vln_b))
+                            st.g(L.vln_b), drop_dy=drops[1])
             _wgrad(dvpre, vout, st.g(L.v_w))
             _colsum(dvpre, st.g(L.v_b))
             dvout = _dgrad(dvpre, st.wt(L.v_w))
-        return dvout, None, None, None, None, None, None, None, None, None, None
+        return dvout, None, None, None, None, None, None, None, None, None, None, None
 
 
 # ================================================================================================
@@ -392,15 +429,17 @@ class LayerNormFn(torch.autograd.Function):
 
 class SmallAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, key_bias, heads):
+    def forward(ctx, q, k, v, key_bias, heads, drop=None):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         B, T, D = q.shape
         d = D // heads
         out = torch.empty_like(q)
         probs = torch.empty(B, heads, T, T, device=q.device)
-        N.small_attn_fwd(B, T, heads, d, q, k, v, key_bias, 1.0 / math.sqrt(d), out, probs)
+        N.small_attn_fwd(B, T, heads, d, q, k, v, key_bias, 1.0 / math.sqrt(d), out, probs,
+                         drop=drop)
         ctx.save_for_backward(q, k, v, probs)
         ctx.heads = heads
+        ctx.drop = drop
         return out
 
     @staticmethod
@@ -410,21 +449,22 @@ class SmallAttnFn(torch.autograd.Function):
         d = D // ctx.heads
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         N.small_attn_bwd(B, T, ctx.heads, d, q, k, v, probs, dout.contiguous(), 1.0 / math.sqrt(d),
-                         dq, dk, dv)
-        return dq, dk, dv, None, None
+                         dq, dk, dv, drop=ctx.drop)
+        return dq, dk, dv, None, None, None
 
 
 class SpanPoolFn(torch.autograd.Function):
     """HierarchicalAttention span pooling over the text rows of the joint output."""
 
     @staticmethod
-    def forward(ctx, top, score, sep):
+    def forward(ctx, top, score, sep, drop=None):
         P, Lt, H = top.shape
         top = top.contiguous()
         probs = torch.empty(P, 2, Lt, device=top.device)
         mix = torch.empty(P, 2, H, device=top.device)
-        N.span_pool_fwd(P, Lt, H, top, Lt * H, score.contiguous(), sep, probs, mix)
+        N.span_pool_fwd(P, Lt, H, top, Lt * H, score.contiguous(), sep, probs, mix, drop=drop)
         ctx.save_for_backward(top, probs, sep)
+        ctx.drop = drop
         return mix
 
     @staticmethod
@@ -433,8 +473,32 @@ class SpanPoolFn(torch.autograd.Function):
         P, Lt, H = top.shape
         dscore = torch.empty(P, Lt, device=top.device)
         dtop = torch.zeros_like(top)
-        N.span_pool_bwd(P, Lt, H, top, Lt * H, probs, sep, dmix.contiguous(), dscore, dtop)
-        return dtop, dscore, None
+        N.span_pool_bwd(P, Lt, H, top, Lt * H, probs, sep, dmix.contiguous(), dscore, dtop,
+                        drop=ctx.drop)
+        return dtop, dscore, None, None
+
+
+class DropoutFn(torch.autograd.Function):
+    """y = dropout(x) with a counter-based mask (the head's nn.Dropout sites); the backward
+    applies the same mask to dy."""
+
+    @staticmethod
+    def forward(ctx, x, drop):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        N.dropout(x, y, drop)
+        ctx.drop = drop
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.empty_like(dy, memory_format=torch.contiguous_format)
+        N.dropout(dy.contiguous(), dx, ctx.drop)
+        return dx, None
+
+
+def dropout(x, drop):
+    return x if drop is None else DropoutFn.apply(x, drop)
 
 
 class PointerFn(torch.autograd.Function):

@@ -34,14 +34,17 @@ class LXRTConfig(SimpleNamespace):
 
     def __init__(self, vocab_size=50265, hidden_size=768, num_hidden_layers=12,
                  num_attention_heads=12, intermediate_size=3072, max_position_embeddings=514,
-                 type_vocab_size=1, hidden_act="gelu", initializer_range=0.02, **kw):
+                 type_vocab_size=1, hidden_act="gelu", initializer_range=0.02,
+                 hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1, **kw):
         super().__init__(vocab_size=vocab_size, hidden_size=hidden_size,
                          num_hidden_layers=num_hidden_layers,
                          num_attention_heads=num_attention_heads,
                          intermediate_size=intermediate_size,
                          max_position_embeddings=max_position_embeddings,
                          type_vocab_size=type_vocab_size, hidden_act=hidden_act,
-                         initializer_range=initializer_range, **kw)
+                         initializer_range=initializer_range,
+                         hidden_dropout_prob=hidden_dropout_prob,
+                         attention_probs_dropout_prob=attention_probs_dropout_prob, **kw)
 
 
 def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25):
@@ -126,6 +129,14 @@ class LXRTModel(nn.Module):
         attach_tree(self, self.store.params)
         self._anchor = torch.zeros((), device=device, requires_grad=True)
         self._build_refs()
+        self.dropout_seed = kw.get("seed", 0)  # fold the rank in for data parallel (trainer.py)
+        self._n_fwd = 0
+
+    def new_dropouts(self):
+        """Fresh dropout descriptors for one forward pass (eval mode: all disabled)."""
+        self._n_fwd += 1
+        seed = (self.dropout_seed * 0x9E3779B97F4A7C15 + self._n_fwd) & ((1 << 64) - 1)
+        return K.Dropouts(seed, self.training)
 
     # -- parameter groups per layer ---------------------------------------------------------
     def _build_refs(self):
@@ -173,7 +184,7 @@ class LXRTModel(nn.Module):
         self.store.set_compute_dtype(dtype)
 
     # -- forward ----------------------------------------------------------------------------
-    def visual_forward(self, images, pairs_list):
+    def visual_forward(self, images, pairs_list):  # CLIP ViT has no dropout (clip/model.py)
         """CLIP ViT over the paired images of every ordered pair (img_len = 2):
         images [B][N][3][R][R] f32 (device), pairs_list [B][npair][2] -> [P*Tv][E]."""
         st = self.store
@@ -191,10 +202,13 @@ class LXRTModel(nn.Module):
         return K.VitProjFn.apply(h, self._anchor, self.proj_refs), Tv
 
     def encode_joint(self, input_ids, attention_mask, token_type_ids=None, images=None,
-                     pairs_list=None):
+                     pairs_list=None, drops=None):
         """Run embeddings (+ ViT + visn_fc) and the joint BERT stack.
         Returns the joint activation [P][T][H] (compute dtype) and Lt."""
         st = self.store
+        D = drops or self.new_dropouts()
+        ph = self.config.hidden_dropout_prob
+        pa = self.config.attention_probs_dropout_prob
         if st.shadow_stale:
             st.refresh_shadows()
         P, Lt = input_ids.shape
@@ -208,10 +222,13 @@ class LXRTModel(nn.Module):
         T = Lt + Tv
         x, key_bias = K.JointInputFn.apply(vout, input_ids.contiguous(), token_type_ids.contiguous(),
                                            attention_mask, self._anchor, self.input_refs, P, Lt,
-                                           Tv, 1e-12, st.compute_dtype)
+                                           Tv, 1e-12, st.compute_dtype,
+                                           (D.site(ph, "emb"), D.site(ph, "visn_fc")))
         heads = self.config.num_attention_heads
-        for L in self.layer_refs:
-            x = K.BertLayerFn.apply(x, key_bias, self._anchor, L, P, T, heads, 1e-12)
+        for i, L in enumerate(self.layer_refs):
+            x = K.BertLayerFn.apply(x, key_bias, self._anchor, L, P, T, heads, 1e-12,
+                                    (D.site(pa, "att", i), D.site(ph, "att_out", i),
+                                     D.site(ph, "out", i)))
         return x.view(P, T, -1), Lt
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, visual_feats=None,

@@ -19,6 +19,7 @@ def run_smoke():
     meta, d, params = load_fixture("tiny")
     m = model_zoo.build_from_golden(meta["config"], device="cuda:0", dtype=torch.float32)
     m.load_state_dict(params)
+    m.eval()  # eval-mode loss is what the oracle restates (dropout off)
     m.zero_grad()
     inputs = {"input_ids": torch.from_numpy(d["input_ids"]), "labels": torch.from_numpy(d["labels"]),
               "images": torch.from_numpy(d["images"]).cuda()}

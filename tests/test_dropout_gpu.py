@@ -1,0 +1,223 @@
+"""Train-mode dropout (include/mmseq.h `mmseq_dropout`): every fused site against an fp32 PyTorch
+reference that applies the SAME counter-based mask, materialised with `mmseq_dropout_apply` on
+a tensor of ones laid out like the site's element index.
+
+The reference draws masks from torch's RNG (nn.Dropout), so bit-equal masks are not expected;
+parity is (i) mask statistics (rate p, kept values scaled 1/(1-p), independent streams) and
+(ii) every kernel's fwd/bwd equals the undropped math with that mask inserted where nn.Dropout
+sits in the reference module (lxrt/modeling.py:369,419,437,491,601; modeling_bert.py:735;
+neural.py:31-32,228; encoder.py:28).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from multimodal_sequencing_amd import _native as nat
+
+DEV = "cuda"
+
+
+def _mask(shape, d):
+    ones = torch.ones(shape, device=DEV)
+    out = torch.empty_like(ones)
+    nat.dropout(ones, out, d)
+    return out
+
+
+def test_mask_statistics_and_streams():
+    n = 1 << 22
+    d = nat.drop(0.1, 7, 12345)
+    m = _mask(n, d)
+    dropped = (m == 0).float().mean().item()
+    assert abs(dropped - 0.1) < 0.002
+    kept = m[m != 0]
+    torch.testing.assert_close(kept, torch.full_like(kept, 1 / 0.9))
+    assert torch.equal(m, _mask(n, d))  # regenerated bit-exactly
+    m2 = _mask(n, nat.drop(0.1, 8, 12345))
+    m3 = _mask(n, nat.drop(0.1, 7, 12346))
+    for o in (m2, m3):  # independent: P(both dropped) ~ p^2
+        both = ((m == 0) & (o == 0)).float().mean().item()
+        assert abs(both - 0.01) < 0.001
+    # bf16 applies the same mask
+    xb = torch.ones(n, device=DEV, dtype=torch.bfloat16)
+    yb = torch.empty_like(xb)
+    nat.dropout(xb, yb, d)
+    assert torch.equal(yb == 0, m == 0)
+    # p = 0 -> no descriptor -> identity
+    assert nat.drop(0.0, 1, 1) is None
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("fast", [1, 3, 0, 4])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (512, 768, 768)])
+def test_gemm_epilogue_dropout(dtype, fast, M, N, K):
+    nat.gemm_set_fast(fast)
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    A = torch.randn(M, K, generator=g).to(DEV, dtype)
+    Bm = (torch.randn(N, K, generator=g) * 0.1).to(DEV, dtype)
+    bias = torch.randn(N, generator=g).to(DEV)
+    resid = torch.randn(M, N, generator=g).to(DEV, dtype)
+    d = nat.drop(0.1, 3, 99)
+    C = torch.empty(M, N, device=DEV, dtype=dtype)
+    nat.gemm(A, Bm, C, M, N, K, bias=bias, resid=resid, drop=d)
+    ref = (A.float() @ Bm.float().t() + bias) * _mask((M, N), d) + resid.float()
+    tol = 2e-5 if dtype == torch.float32 else 3e-2
+    err = (C.float() - ref).abs().max().item()
+    assert err <= tol * (1 + ref.abs().max().item()) * math.sqrt(K) / 8
+    nat.gemm_set_fast(1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_dropout_fwd_bwd(dtype):
+    rows, cols = 257, 768
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(rows, cols, generator=g).to(DEV, dtype)
+    gamma = (1 + 0.1 * torch.randn(cols, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(cols, generator=g)).to(DEV)
+    dy_ = nat.drop(0.1, 21, 5)
+    dx_ = nat.drop(0.1, 22, 5)
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    nat.layernorm_fwd(rows, cols, x, nat.rows(cols), gamma, beta, 1e-12, y, nat.rows(cols), mean,
+                      rstd, drop=dy_)
+    My, Mx = _mask((rows, cols), dy_), _mask((rows, cols), dx_)
+    xf = x.float().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xf, (cols,), gamma, beta, 1e-12) * My
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol * 4)
+    dy = torch.randn(rows, cols, generator=g).to(DEV, dtype)
+    dx = torch.empty_like(x)
+    dxd = torch.empty_like(x)
+    dg, db = torch.zeros_like(gamma), torch.zeros_like(beta)
+    nat.layernorm_bwd(rows, cols, dy, nat.rows(cols), x, nat.rows(cols), mean, rstd, gamma, dx,
+                      nat.rows(cols), None, nat.rows(cols), dg, db, drop_dy=dy_, dx_drop=dxd,
+                      drop_dx=dx_)
+    (rdx,) = torch.autograd.grad(ref, xf, dy.float())
+    torch.testing.assert_close(dx.float(), rdx, rtol=tol, atol=tol * 4)
+    torch.testing.assert_close(dxd.float(), dx.float() * Mx, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("P,T,heads,masked", [(2, 129, 2, True), (1, 513, 3, True),
+                                              (2, 64, 1, False)])
+def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked):
+    g = torch.Generator(device="cpu").manual_seed(T + heads)
+    H = heads * 64
+    qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, dtype)
+    bias = None
+    if masked:
+        m = (torch.rand(P, T, generator=g) > 0.3).float()
+        m[:, 0] = 1
+        bias = ((1 - m) * -10000.0).to(DEV)
+    d = nat.drop(0.1, 5, 2024)
+    scale = 1 / 8
+    out = torch.empty(P * T, H, device=DEV, dtype=dtype)
+    lse = torch.empty(P, heads, T, device=DEV)
+    nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse, drop=d)
+    Mk = _mask((P, heads, T, T), d)
+    qf = qkv.float().requires_grad_(True)
+    q, k, v = qf.view(P, T, 3, heads, 64).unbind(2)
+    s = torch.einsum("pqhd,pkhd->phqk", q, k) * scale
+    if bias is not None:
+        s = s + bias[:, None, None, :]
+    a = torch.softmax(s, -1) * Mk
+    ref = torch.einsum("phqk,pkhd->pqhd", a, v).reshape(P * T, H)
+    tol = 3e-5 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+    dout = torch.randn(P * T, H, generator=g).to(DEV, dtype)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(P, heads, T, device=DEV)
+    nat.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, dout, H, lse, delta,
+                 dqkv, 3 * H, drop=d)
+    (rg,) = torch.autograd.grad(ref, qf, dout.float())
+    torch.testing.assert_close(dqkv.float(), rg, rtol=2 * tol, atol=2 * tol)
+
+
+def test_small_attention_dropout():
+    B, T, heads, d = 3, 7, 4, 16
+    g = torch.Generator(device="cpu").manual_seed(3)
+    q, k, v = (torch.randn(B, T, heads * d, generator=g).to(DEV) for _ in range(3))
+    m = torch.ones(B, T)
+    m[1, 4:] = 0
+    bias = ((1 - m) * -10000.0).to(DEV)
+    dr = nat.drop(0.1, 9, 77)
+    out = torch.empty_like(q)
+    probs = torch.empty(B, heads, T, T, device=DEV)
+    nat.small_attn_fwd(B, T, heads, d, q, k, v, bias, d ** -0.5, out, probs, drop=dr)
+    Mk = _mask((B, heads, T, T), dr)
+    qf, kf, vf = (t.clone().requires_grad_(True) for t in (q, k, v))
+    s = torch.einsum("bqhd,bkhd->bhqk", qf.view(B, T, heads, d), kf.view(B, T, heads, d)) * d ** -0.5
+    a = torch.softmax(s + bias[:, None, None, :], -1) * Mk
+    ref = torch.einsum("bhqk,bkhd->bqhd", a, vf.view(B, T, heads, d)).reshape(B, T, heads * d)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    do = torch.randn_like(q)
+    dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+    nat.small_attn_bwd(B, T, heads, d, q, k, v, probs, do, d ** -0.5, dq, dk, dv, drop=dr)
+    for a_, b_ in zip((dq, dk, dv), torch.autograd.grad(ref, (qf, kf, vf), do)):
+        torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-5)
+
+
+def test_span_pool_dropout():
+    P, Lt, H = 5, 19, 64
+    g = torch.Generator(device="cpu").manual_seed(8)
+    top = torch.randn(P, Lt, H, generator=g).to(DEV)
+    score = torch.randn(P, Lt, generator=g).to(DEV)
+    sep = torch.tensor([[3, 9], [7, 18], [1, 2], [5, 12], [2, 18]], device=DEV)
+    dr = nat.drop(0.1, 4, 31)
+    probs = torch.empty(P, 2, Lt, device=DEV)
+    mix = torch.empty(P, 2, H, device=DEV)
+    nat.span_pool_fwd(P, Lt, H, top, Lt * H, score, sep, probs, mix, drop=dr)
+    Mk = _mask((P, 2, Lt), dr)
+    tf = top.clone().requires_grad_(True)
+    sf = score.clone().requires_grad_(True)
+    pos = torch.arange(Lt, device=DEV)[None]
+    m0 = ((pos >= 1) & (pos <= sep[:, :1])).float()
+    m1 = ((pos > sep[:, :1]) & (pos <= sep[:, 1:])).float()
+    sel = torch.stack([m0, m1], 1)
+    a = torch.softmax(sel * sf[:, None] + (1 - sel) * -10000.0, -1) * Mk
+    ref = a @ tf
+    torch.testing.assert_close(mix, ref, rtol=1e-5, atol=1e-5)
+    dmix = torch.randn(P, 2, H, generator=g).to(DEV)
+    dscore = torch.empty(P, Lt, device=DEV)
+    dtop = torch.zeros_like(top)
+    nat.span_pool_bwd(P, Lt, H, top, Lt * H, probs, sep, dmix, dscore, dtop, drop=dr)
+    rt, rs = torch.autograd.grad(ref, (tf, sf), dmix)
+    torch.testing.assert_close(dtop, rt, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dscore, rs, rtol=1e-4, atol=1e-5)
+
+
+def test_embed_ln_dropout_equals_masked_undropped():
+    P, Lt, Tv, H, V = 3, 11, 4, 128, 40
+    T = Lt + Tv
+    g = torch.Generator(device="cpu").manual_seed(6)
+    ids = torch.randint(0, V, (P, Lt), generator=g).to(DEV)
+    tt = torch.zeros(P, Lt, dtype=torch.long, device=DEV)
+    word = torch.randn(V, H, generator=g).to(DEV)
+    pos = torch.randn(20, H, generator=g).to(DEV)
+    typ = torch.randn(1, H, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(H, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(H, generator=g)).to(DEV)
+    dr = nat.drop(0.1, 12, 3)
+    outs, grads = [], []
+    dj = torch.randn(P, T, H, generator=g).to(DEV)
+    Mk = _mask((P, Lt, H), dr)
+    for d, djm in ((dr, dj), (None, None)):
+        joint = torch.zeros(P, T, H, device=DEV)
+        mean, rstd = torch.empty(P * Lt, device=DEV), torch.empty(P * Lt, device=DEV)
+        nat.embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gam, bet, 1e-12, joint, T * H, mean,
+                         rstd, drop=d)
+        if djm is None:  # undropped kernel fed the masked gradient
+            djm = dj.clone()
+            djm[:, :Lt] *= Mk
+        gs = [torch.zeros_like(t) for t in (word, pos, typ, gam, bet)]
+        nat.embed_ln_bwd(P, Lt, H, ids, tt, word, pos, typ, gam, mean, rstd, djm, T * H, *gs,
+                         drop=d)
+        outs.append(joint[:, :Lt].clone())
+        grads.append(gs)
+    torch.testing.assert_close(outs[0], outs[1] * Mk, rtol=1e-6, atol=1e-6)
+    for a_, b_ in zip(*grads):
+        torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-5)

@@ -34,7 +34,7 @@ def _q(x, dtype):
 @pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 200, 136), (77, 96, 520), (1, 2, 768),
                                    (513, 768, 768)])
 @pytest.mark.parametrize("act", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", [1, 3, 0, 4])
 def test_gemm_nt_epilogues(dtype, M, N, K, act, fast):
     nat.gemm_set_fast(fast)
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + act)
@@ -57,7 +57,7 @@ def test_gemm_nt_epilogues(dtype, M, N, K, act, fast):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 96, 300), (768, 768, 1026), (2, 520, 77),
                                    (768, 3072, 4100), (136, 264, 64)])
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", [1, 3, 0])
 def test_gemm_tn_accumulate(dtype, M, N, K, fast):
     nat.gemm_set_fast(fast)
     # dW[M][N] += sum_k dY[k][M] X[k][N]  (wgrad layout)
@@ -73,7 +73,7 @@ def test_gemm_tn_accumulate(dtype, M, N, K, fast):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_dact_and_batched(dtype):
-    nat.gemm_set_fast(True)
+    nat.gemm_set_fast(1)
     g = torch.Generator(device="cpu").manual_seed(3)
     M, Nn, K, Bt = 96, 64, 128, 3
     A = torch.randn(Bt, M, K, generator=g).to(DEV, dtype)
@@ -89,7 +89,7 @@ def test_gemm_dact_and_batched(dtype):
 
 def test_gemm_fast_strided_batched():
     # batched NT with a row stride > K and non-multiple-of-128 M (visn_fc into the joint rows)
-    nat.gemm_set_fast(True)
+    nat.gemm_set_fast(1)
     Bt, M, K, Nn, ldc = 3, 200, 128, 192, 192
     g = torch.Generator(device="cpu").manual_seed(9)
     A = torch.randn(Bt, M, K, generator=g).to(DEV, torch.bfloat16)
@@ -99,6 +99,38 @@ def test_gemm_fast_strided_batched():
     ref = A.float() @ W.float().t()
     _close(C[:, 50:], ref, torch.bfloat16, scale=2.0)
     assert C[:, :50].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("fast", [1, 4])
+def test_gemm_big_tile_path(fast):
+    # >= 512 256x256 tiles selects the 256^2 NT kernel by default; ragged M edge, GELU + aux +
+    # residual epilogue; mode 4 also runs it batched with strides
+    nat.gemm_set_fast(fast)
+    M, Nn, K = 33000 + 77, 1024, 256
+    g = torch.Generator(device="cpu").manual_seed(10)
+    A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(Nn, K, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(Nn, generator=g).to(DEV)
+    resid = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    C = torch.empty(M, Nn, device=DEV, dtype=torch.bfloat16)
+    aux = torch.empty_like(C)
+    nat.gemm(A, W, C, M, Nn, K, bias=bias, act=1, aux=aux, resid=resid)
+    z = A.float() @ W.float().t() + bias
+    _close(aux, z, torch.bfloat16, scale=2.0)
+    _close(C, torch.nn.functional.gelu(z) + resid.float(), torch.bfloat16, scale=2.0)
+    if fast == 4:
+        Bt, Mb = 3, 300
+        Ab = torch.randn(Bt, Mb, K, generator=g).to(DEV, torch.bfloat16)
+        Cb = torch.zeros(Bt, Mb + 20, Nn, device=DEV, dtype=torch.bfloat16)
+        nat.gemm(Ab, W, Cb[:, 20:], Mb, Nn, K, batch=Bt, sA=Mb * K, sC=(Mb + 20) * Nn)
+        _close(Cb[:, 20:], Ab.float() @ W.float().t(), torch.bfloat16, scale=2.0)
+        assert Cb[:, :20].abs().max().item() == 0
+
+
+@pytest.fixture(autouse=True)
+def _restore_gemm_path():
+    yield
+    nat.gemm_set_fast(1)
 
 
 def _attn_ref(qkv, P, T, heads, bias, scale):

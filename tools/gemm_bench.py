@@ -25,5 +25,15 @@ R = 164160  # joint rows at 16 stories (320 pairs x 513)
 shapes = [(R, 2304, 768, 0), (R, 768, 768, 0), (R, 3072, 768, 0), (R, 768, 3072, 0),
           (768, 3072, R, 1), (3072, 768, R, 1), (2304, 768, R, 1), (768, 768, R, 1), (4096, 4096, 4096, 0), (4096, 4096, 4096, 1)]
 for M, Nn, K, tr in shapes:
-    f = bench(M, Nn, K, tr, True); g = bench(M, Nn, K, tr, False)
-    print(json.dumps({"M": M, "N": Nn, "K": K, "trans": tr, "fast_tflops": round(f, 1), "generic_tflops": round(g, 1)}), flush=True)
+    modes = (("default", 1), ("big", 4), ("dbuf", 2), ("ring", 3)) if not tr else \
+        (("default", 1), ("dbuf", 2), ("ring", 3))
+    r = {k: round(bench(M, Nn, K, tr, v), 1) for k, v in modes}
+    if tr == 0:  # hipBLASLt through torch, as a yardstick only
+        A = torch.randn(M, K, device="cuda").bfloat16(); B = torch.randn(Nn, K, device="cuda").bfloat16()
+        for _ in range(3): torch.matmul(A, B.t())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10): torch.matmul(A, B.t())
+        e1.record(); torch.cuda.synchronize()
+        r["torch"] = round(2.0 * M * Nn * K / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e12, 1)
+    print(json.dumps({"M": M, "N": Nn, "K": K, "trans": tr, **r}), flush=True)
