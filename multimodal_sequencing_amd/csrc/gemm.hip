@@ -15,7 +15,7 @@
 // for the fused epilogue (bias, activation / activation-backward, residual, accumulate).
 // Staging: global -> registers (16 B per lane per chunk, issued before the MFMA loop of the
 // previous tile) -> LDS after the barrier (the async-STAGE split of the guide, T14).
-#include "common.h"
+#include "gemm_common.h"
 
 static int g_disable_fast = 0;  // test hook: force the generic kernel
 // caller-provided split-K slab workspace (mmseq_gemm_set_workspace); stream-ordered use only
@@ -23,8 +23,10 @@ static float* g_slab = nullptr;
 static int g_ring = 0;  // 1: BK=32 four-slot ring kernel, 0: BK=64 double-buffer kernel
 static int g_big = 1;   // 256 x 256 NT kernel: 1 for large problems, 2 always (tests)
 static int64_t g_slab_bytes = 0;
+static int g_num_cu = 256;  // persistent grid size (set from the device at first use)
 
 namespace {
+using namespace mmseq_gemm_detail;
 
 constexpr int BM = 128, BN = 128, NT_THREADS = 256;
 
@@ -38,17 +40,6 @@ template <> struct Cfg<float> {
   static constexpr int BK = 32, VE = 4;
   static constexpr int PADK = 4;   // NT row = 36 floats
   static constexpr int PADM = 4;   // TN row = 132 floats
-};
-
-struct GemmArgs {
-  int M, N, K;
-  const void* A; int64_t lda, sA;
-  const void* B; int64_t ldb, sB;
-  void* C; int64_t ldc, sC;
-  const float* bias; int act; void* aux; const void* dact; const void* resid; int64_t ldr, sR;
-  float alpha; int accumulate; int vec_ok; int vec_c;
-  int splitk; int kchunk; float* slab;  // split-K (TN wgrad): partial slabs [splitk][M][N] f32
-  Drop drop;                            // dropout after the activation, before the residual
 };
 
 template <typename TI, bool TRANS>
@@ -135,65 +126,6 @@ __device__ __forceinline__ bf16x8_t frag_tn_bf16(const unsigned short* s, int rb
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, v);
-}
-
-template <typename TO>
-__device__ __forceinline__ void epilogue4(const GemmArgs& a, TO* __restrict__ C, const TO* resid,
-                                          TO* aux, const TO* dact, int m, int n, const float* acc,
-                                          int b = 0) {
-  if (m >= a.M || n >= a.N) return;
-  float v[4];
-  bool full = (n + 3 < a.N);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = acc[r] * a.alpha;
-    if (a.bias && n + r < a.N) v[r] += a.bias[n + r];
-  }
-  TO* cp = C + (int64_t)m * a.ldc + n;
-  if (dact) {
-    const TO* dp = dact + (int64_t)m * a.ldc + n;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < a.N) v[r] *= act_bwd(a.act, Elem<TO>::ld(dp + r));
-  } else if (a.act) {
-    TO* ap = aux ? aux + (int64_t)m * a.ldc + n : nullptr;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (n + r < a.N) {
-        if (ap) Elem<TO>::st(ap + r, v[r]);
-        v[r] = act_fwd(a.act, v[r]);
-      }
-    }
-  }
-  if (a.drop.thr) {
-    const int64_t di = ((int64_t)b * a.M + m) * a.N + n;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= drop_mul(a.drop, di + r);
-  }
-  if (resid) {
-    const TO* rp = resid + (int64_t)m * a.ldr + n;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < a.N) v[r] += Elem<TO>::ld(rp + r);
-  }
-  if (a.accumulate) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < a.N) v[r] += Elem<TO>::ld(cp + r);
-  }
-  if (full && a.vec_c) {
-    if (sizeof(TO) == 2) {
-      u16x4 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-      *reinterpret_cast<u16x4*>(cp) = o;
-    } else {
-      f32x4 o = {v[0], v[1], v[2], v[3]};
-      *reinterpret_cast<f32x4*>(cp) = o;
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < a.N) Elem<TO>::st(cp + r, v[r]);
-  }
 }
 
 template <typename TI, typename TO, bool TRANS>
@@ -333,17 +265,6 @@ hipError_t launch(int trans, const GemmArgs& a, int batch, hipStream_t s) {
 //   TN image: [64 k][128 m], 256-B rows, chunk' = chunk ^ ((row & 7) << 1)     -> conflict-free
 //             ds_read_b64_tr_b16 (each 32-lane half reads 8 rows x 2 chunks = 16 slots)
 // =============================================================================================
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
-  uint32_t n = bytes <= 0 ? 0u : (bytes >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
-}
-
-__device__ __forceinline__ void dma16(rsrc_t r, unsigned short* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMSEQ_LDS void*)lds, 16, voff, 0, 0, 0);
-}
-
 template <bool TRANS>
 __device__ __forceinline__ bf16x8_t frag_swz(const unsigned short* s, int rb, int ks, int lane) {
   if (!TRANS) {
@@ -629,107 +550,6 @@ __global__ __launch_bounds__(256, 2) void gemm_ring_kernel(GemmArgs a, int tiles
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Large NT kernel (forward / dgrad over the 164k-row activations): 256 x 256 output tile,
-// 8 waves (2 along M x 4 along N, 128 x 64 each = 8 x 4 MFMA 16x16 tiles), BK = 64, one block
-// per CU. Per K-step the block reads 64 KB of operands into LDS and every wave reads 24 KB of
-// fragments (A 16 KB + B 8 KB): 1536 LDS cycles against 2048 MFMA cycles per SIMD pair, where
-// the 128 x 128 tile needs 100 % of the LDS port (the ~900 TF ceiling of guide §5).
-// Pipeline: two 64 KB buffers, K-tile t + 2 is staged (LDS-DMA, swizzled images as in the
-// 128 x 128 NT path) as soon as every wave has read K-tile t's fragments; the wait for a K-tile
-// is a COUNTED vmcnt (the next K-tile's 8 DMAs per lane stay in flight) and raw s_barriers.
-// ---------------------------------------------------------------------------------------------
-template <typename TO>
-__global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 4 * 8192];  // 128 KB
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nwg = gridDim.x, L = blockIdx.x;
-  const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int Lr = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-  const int tm = Lr / tiles_n, tn = Lr % tiles_n;
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int b = blockIdx.y;
-  const unsigned short* A = reinterpret_cast<const unsigned short*>(a.A) + (int64_t)b * a.sA;
-  const unsigned short* B = reinterpret_cast<const unsigned short*>(a.B) + (int64_t)b * a.sB;
-  const rsrc_t ra = make_rsrc(A + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
-  const rsrc_t rb = make_rsrc(B + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // half-tiles: 0 = A rows 0..127, 1 = A rows 128..255, 2/3 = B likewise; 2 DMAs per lane each
-  auto issue = [&](int kt, int buf) {
-    const int k0 = kt * 64;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      unsigned short* sh = smem + (buf * 4 + h) * 8192;
-      const int64_t ld = h < 2 ? a.lda : a.ldb;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int inst = wave * 2 + i;
-        const int row = inst * 8 + (lane >> 3), cp = lane & 7;
-        const int c = cp ^ ((row >> 1) & 7);
-        const uint32_t voff = (uint32_t)((((int64_t)((h & 1) * 128 + row)) * ld + k0 + c * 8) * 2);
-        dma16(h < 2 ? ra : rb, sh + inst * 512, voff);
-      }
-    }
-  };
-
-  const int nk = a.K / 64;
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  for (int t = 0; t < nk; ++t) {
-    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // K-tile t landed for every wave
-    asm volatile("" ::: "memory");
-    const unsigned short* sA = smem + ((t & 1) * 4 + wr) * 8192;
-    const unsigned short* sB = smem + ((t & 1) * 4 + 2 + (wc >> 1)) * 8192;
-    bf16x8_t fa[2][8], fb[2][4];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[ks][j] = frag_swz<false>(sB, (wc & 1) * 64 + j * 16, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) fa[ks][i] = frag_swz<false>(sA, i * 16, ks, lane);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j], fa[0][i], acc[i][j], 0, 0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave holds K-tile t in registers: buffer t & 1 free
-    asm volatile("" ::: "memory");
-    if (t + 2 < nk) issue(t + 2, t & 1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j], fa[1][i], acc[i][j], 0, 0, 0);
-  }
-
-  const int g = lane >> 4, ii = lane & 15;
-  TO* C = reinterpret_cast<TO*>(a.C) + (int64_t)b * a.sC;
-  const TO* resid = a.resid ? reinterpret_cast<const TO*>(a.resid) + (int64_t)b * a.sR : nullptr;
-  TO* aux = a.aux ? reinterpret_cast<TO*>(a.aux) + (int64_t)b * a.sC : nullptr;
-  const TO* dact = a.dact ? reinterpret_cast<const TO*>(a.dact) + (int64_t)b * a.sC : nullptr;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int m = m0 + wr * 128 + i * 16 + ii;
-      int n = n0 + wc * 64 + j * 16 + 4 * g;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epilogue4<TO>(a, C, resid, aux, dact, m, n, v, b);
-    }
-}
-
 // C[m][n] (+)= sum_s slab[s][m][n], fixed order (bitwise reproducible)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S, const float* __restrict__ slab,
                                                             float* __restrict__ C, int64_t ldc,
@@ -748,12 +568,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 
 template <typename TO>
 hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s) {
-  if (!trans && g_big && a.splitk == 1 &&
-      (g_big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) * batch >= 512)) {
-    const int tn = (a.N + 255) / 256;
-    dim3 grid(((a.M + 255) / 256) * tn, batch);
-    hipLaunchKernelGGL((gemm256_nt_kernel<TO>), grid, dim3(512), 0, s, a, tn);
-    return hipGetLastError();
+  if (!trans && g_big && a.splitk == 1 && batch == 1 && a.K % 128 == 0 &&
+      (g_big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256)) {
+    hipError_t e;
+    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, g_num_cu, s, &e)) return e;
   }
   const int tiles_m = (a.M + 127) / 128, tiles_n = (a.N + 127) / 128;
   dim3 grid(tiles_m * tiles_n, a.splitk > 1 ? a.splitk : batch);
@@ -808,6 +626,14 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
     MMSEQ_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gemm TN: ld too small");
   }
   if (M == 0 || N == 0) return MMSEQ_OK;
+  static int cu_init = 0;
+  if (!cu_init) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cu = n;
+    cu_init = 1;
+  }
   GemmArgs a;
   a.M = M; a.N = N; a.K = K;
   a.A = A; a.lda = lda; a.sA = strideA;

@@ -1,0 +1,317 @@
+// Persistent 256 x 256 bf16 NT GEMM (forward Y = X W^T and dgrad dX = dY W over the 164k-row
+// activations of the joint encoder and the ViT); see gemm_common.h for the shared epilogue.
+#include "gemm_common.h"
+
+using namespace mmseq_gemm_detail;
+
+namespace {
+
+// Compile-time-specialised epilogue for the 256 x 256 kernel: one lane owns 8 contiguous outputs
+// of a row (two 16x16 tiles whose B rows are interleaved, see the kernel), so every access is
+// 16 bytes. bf16 out; the host guarantees N % 8 == 0, ldc % 8 == 0, ldr % 8 == 0 and 16-byte
+// aligned C / aux / dact / resid. Specialised per activation so the 16 unrolled copies stay small.
+typedef unsigned short us;
+__device__ __forceinline__ void ld8(const us* p, float* v) {
+  const u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = bf2f(u[r]);
+}
+__device__ __forceinline__ void st8(us* p, const float* v) {
+  u16x8 u;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) u[r] = f2bf(v[r]);
+  *reinterpret_cast<u16x8*>(p) = u;
+}
+
+template <int ACT, bool BWD>
+__device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi) {
+  if (m >= a.M || n >= a.N) return;
+  float v[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { v[r] = lo[r] * a.alpha; v[4 + r] = hi[r] * a.alpha; }
+  if (a.bias) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += a.bias[n + r];
+  }
+  const int64_t off = (int64_t)m * a.ldc + n;
+  if (BWD) {
+    float d[8];
+    ld8(reinterpret_cast<const us*>(a.dact) + off, d);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] *= act_bwd(ACT, d[r]);
+  } else if (ACT) {
+    if (a.aux) st8(reinterpret_cast<us*>(a.aux) + off, v);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd(ACT, v[r]);
+  }
+  if (a.drop.thr) {
+    const int64_t di = (int64_t)m * a.N + n;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] *= drop_mul(a.drop, di + r);
+  }
+  if (a.resid) {
+    float t[8];
+    ld8(reinterpret_cast<const us*>(a.resid) + (int64_t)m * a.ldr + n, t);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += t[r];
+  }
+  us* cp = reinterpret_cast<us*>(a.C) + off;
+  if (a.accumulate) {
+    float t[8];
+    ld8(cp, t);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += t[r];
+  }
+  st8(cp, v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large NT kernel (forward / dgrad over the 164k-row activations): persistent 256 x 256 tiles,
+// 8 waves (2 along M x 4 along N, 128 x 64 outputs each = 8 x 4 MFMA 16x16 tiles), BK = 64,
+// one 512-thread workgroup per CU, the guide's 8-phase schedule (cdna_hip_programming.md §5):
+//  * LDS: two K-tile buffers of 64 KB (A image [256][64] + B image [256][64], 128-B rows),
+//    filled by LDS-DMA with the swizzle on the source (guide rule 21). A: chunk' = chunk ^
+//    ((row >> 1) & 7). B fragments are row-permuted: MFMA row rho of the wave's j-th 16-column
+//    tile reads B row 8 (rho >> 2) + 4 (j & 1) + (rho & 3) + 32 (j >> 1), so after the swapped
+//    MFMA a lane holds 8 CONTIGUOUS outputs of one row across tiles (2t, 2t + 1) -> 16-byte
+//    epilogue accesses; B swizzle chunk' = chunk ^ (((row >> 1) & 1) | (((row >> 3) & 3) << 1))
+//    keeps those permuted 16-row reads conflict-free for the ds_read_b128 lane groups.
+//  * A K-tile is four 16 KB "half-tiles" named by which fragment registers read them:
+//    A_lo (rows 0-63 of each 128-row A half), A_hi, B_lo (rows {0-31, 64-95} of each B half), B_hi.
+//  * Two K-tiles per iteration, four phases each; per phase: ds_read this phase's fragments,
+//    stage one half-tile (2 LDS-DMA per lane), s_barrier, lgkmcnt(0), 16 MFMAs, s_barrier.
+//    Reads: phase 1 A_lo + B_lo, 2 B_hi, 3 A_hi, 4 none (MFMA quadrants q0..q3 snake through
+//    the registers). Waves 4-7 run one barrier behind waves 0-3 (stagger: one group's MFMAs
+//    beside the other group's reads), so a region is restaged >= 2 phases after its last read;
+//    the counted vmcnt(4) before the first barrier of phases 4 and 8 retires the K-tile read
+//    next while two half-tiles stay in flight.
+//  * Staging runs across tile boundaries: the last iteration of a tile stages the NEXT tile's
+//    first K-tiles, so its loads fly during the epilogue (dummy zero-size loads past the end keep
+//    the vmcnt arithmetic uniform). Preconditions (host): bf16, K % 128 == 0, batch 1, no split.
+// ---------------------------------------------------------------------------------------------
+constexpr int G_LDA_HALF = 16384;  // elements per 256 x 64 operand image
+
+// 8-row group (0..31 of the 256-row image) written by wave-instruction q (0..15) of half-tile X
+__device__ __forceinline__ int g8_of(int X, int q) {
+  // X: 0 = A_lo, 1 = B_lo, 2 = B_hi, 3 = A_hi
+  if (X == 0) return (q & 7) + ((q >> 3) << 4);
+  if (X == 3) return 8 + (q & 7) + ((q >> 3) << 4);
+  if (X == 1) return (q & 3) + ((q >> 2) << 3);
+  return 4 + (q & 3) + ((q >> 2) << 3);
+}
+
+template <int ACT, bool BWD>
+__global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int G = gridDim.x;
+  // XCD-aware order: the G/8 blocks sharing an XCD take consecutive tiles (shared A panels in L2)
+  const int bid = blockIdx.x;
+  const int first = (G & 7) == 0 ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  const int nk = a.K >> 6;
+  const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
+  const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);
+
+  // per-lane source offsets (bytes) for a 1 KB piece = 8 rows x 128 B; the swizzle term
+  // ((row >> 1) & 7) = (lane >> 4) | 4 * (g8 & 1) depends on the parity of the 8-row group
+  const int lr = lane >> 3, lc = lane & 7;
+  const uint32_t offA0 = (uint32_t)(lr * a.lda * 2 + ((lc ^ (lane >> 4)) << 4));
+  const uint32_t offA1 = (uint32_t)(lr * a.lda * 2 + ((lc ^ ((lane >> 4) | 4)) << 4));
+  // B: swizzle term ((lane >> 4) & 1) | ((g8 & 3) << 1)
+  const uint32_t offB0 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ ((lane >> 4) & 1)) << 4));
+  const uint32_t offB1 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ (((lane >> 4) & 1) | 2)) << 4));
+  const uint32_t offB2 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ (((lane >> 4) & 1) | 4)) << 4));
+  const uint32_t offB3 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ (((lane >> 4) & 1) | 6)) << 4));
+
+  // stage half-tile X of K-tile kk (relative to tile iteration `it`; kk >= nk means the next tile)
+  auto stage = [&](int it, int kk, int X) {
+    if (kk >= nk) { kk -= nk; ++it; }
+    const int tile = first + it * G;
+    const bool isA = (X == 0 || X == 3);
+    rsrc_t r;
+    if (tile < ntiles) {
+      const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+      if (isA) {
+        const int m0 = tm * 256;
+        r = make_rsrc(Ab + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
+      } else {
+        const int n0 = tn * 256;
+        r = make_rsrc(Bb + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
+      }
+    } else {
+      r = make_rsrc(Ab, 0);  // past the last tile: zero-fill, no traffic
+    }
+    const int64_t ld = isA ? a.lda : a.ldb;
+    unsigned short* img = smem + (kk & 1) * (2 * G_LDA_HALF) + (isA ? 0 : G_LDA_HALF);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = wave * 2 + i;
+      const int g8 = g8_of(X, q);
+      const int gb = g8 & 3;
+      const uint32_t lo = isA ? ((g8 & 1) ? offA1 : offA0)
+                              : (gb == 0 ? offB0 : gb == 1 ? offB1 : gb == 2 ? offB2 : offB3);
+      const uint32_t voff = lo + (uint32_t)((g8 * 8 * ld + kk * 64) * 2);
+      dma16(r, img + g8 * 512, voff);
+    }
+  };
+
+  // fragment read offsets (elements): row = base + l15, chunk (ks * 4 + (lane >> 4)) ^ (l15 >> 1)
+  const int l15 = lane & 15;
+  const int sw0 = ((lane >> 4) ^ (l15 >> 1)) << 3;
+  const int sw1 = ((4 + (lane >> 4)) ^ (l15 >> 1)) << 3;
+  const int arow = (wr * 128 + l15) * 64;
+  const int hb = ((l15 >> 1) & 1) | ((l15 >> 2) << 1);
+  const int swb0 = ((lane >> 4) ^ hb) << 3;
+  const int swb1 = ((4 + (lane >> 4)) ^ hb) << 3;
+  const int brow = G_LDA_HALF + ((wc >> 1) * 128 + (wc & 1) * 64 + 8 * (l15 >> 2) + (l15 & 3)) * 64;
+#define FR(base, t, ks) __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>( \
+      smem + (base) + (t) * 1024 + ((ks) ? sw1 : sw0)))
+#define FRB(base, j, ks) __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>( \
+      smem + (base) + (4 * ((j) & 1) + 32 * ((j) >> 1)) * 64 + ((ks) ? swb1 : swb0)))
+
+  int it = 0;
+  if (first >= ntiles) return;
+  stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2); stage(0, 0, 3);
+  stage(0, 1, 0); stage(0, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+
+  f32x4 acc[8][4];
+  bf16x8_t fa[8][2], fb[4][2];
+  for (int tile = first; tile < ntiles; tile += G, ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int s = 0; s < (nk >> 1); ++s) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // h = 0: even K-tile 2s, h = 1: odd K-tile 2s + 1
+        const int buf = h * (2 * G_LDA_HALF);
+        // ---- phase 1 (5): A_lo + B_lo, quadrant (i 0-3, j 0-1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { fa[i][0] = FR(buf + arow, i, 0); fa[i][1] = FR(buf + arow, i, 1); }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) { fb[j][0] = FRB(buf + brow, j, 0); fb[j][1] = FRB(buf + brow, j, 1); }
+        if (h == 0) stage(it, 2 * s + 1, 2); else stage(it, 2 * s + 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // ---- phase 2 (6): B_hi, quadrant (i 0-3, j 2-3)
+#pragma unroll
+        for (int j = 2; j < 4; ++j) { fb[j][0] = FRB(buf + brow, j, 0); fb[j][1] = FRB(buf + brow, j, 1); }
+        if (h == 0) stage(it, 2 * s + 1, 3); else stage(it, 2 * s + 2, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 2; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // ---- phase 3 (7): A_hi, quadrant (i 4-7, j 2-3)
+#pragma unroll
+        for (int i = 4; i < 8; ++i) { fa[i][0] = FR(buf + arow, i, 0); fa[i][1] = FR(buf + arow, i, 1); }
+        if (h == 0) stage(it, 2 * s + 2, 0); else stage(it, 2 * s + 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 4; i < 8; ++i)
+#pragma unroll
+            for (int j = 2; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // ---- phase 4 (8): no reads, quadrant (i 4-7, j 0-1); retire the K-tile read next
+        if (h == 0) stage(it, 2 * s + 2, 1); else stage(it, 2 * s + 3, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 4; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+
+    // ---- epilogue (the next tile's first K-tiles are already in flight)
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int g = lane >> 4, ii = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        epi8<ACT, BWD>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, acc[i][2 * t],
+                       acc[i][2 * t + 1]);
+  }
+#undef FR
+#undef FRB
+  if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
+}  // namespace
+
+bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s, hipError_t* err) {
+  auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  if (!out_bf16 || a.K % 128 != 0 || a.splitk != 1 || a.N % 8 != 0 || a.ldc % 8 != 0 ||
+      (a.resid && (a.ldr % 8 != 0 || !a16(a.resid))) || !a16(a.C) || (a.aux && !a16(a.aux)) ||
+      (a.dact && !a16(a.dact)))
+    return false;
+  const int tn = (a.N + 255) / 256;
+  const int ntiles = ((a.M + 255) / 256) * tn;
+  const int grid = ntiles < num_cu ? ntiles : num_cu;
+  const dim3 g(grid), b(512);
+  const bool bwd = a.dact != nullptr;
+  switch (a.act) {
+    case 0: hipLaunchKernelGGL((gemm256_nt_kernel<0, false>), g, b, 0, s, a, tn, ntiles); break;
+    case MMSEQ_ACT_GELU_ERF:
+      if (bwd) hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, true>), g, b, 0, s, a, tn, ntiles);
+      else hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, false>), g, b, 0, s, a, tn, ntiles);
+      break;
+    case MMSEQ_ACT_QUICKGELU:
+      if (bwd) hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, true>), g, b, 0, s, a, tn, ntiles);
+      else hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, false>), g, b, 0, s, a, tn, ntiles);
+      break;
+    default: return false;
+  }
+  *err = hipGetLastError();
+  return true;
+}

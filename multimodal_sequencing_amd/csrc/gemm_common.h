@@ -1,0 +1,94 @@
+// Shared pieces of the GEMM kernels (gemm.hip, gemm256.hip): argument block, fused epilogue,
+// buffer-resource LDS-DMA helpers.
+#pragma once
+#include "common.h"
+
+namespace mmseq_gemm_detail {
+
+struct GemmArgs {
+  int M, N, K;
+  const void* A; int64_t lda, sA;
+  const void* B; int64_t ldb, sB;
+  void* C; int64_t ldc, sC;
+  const float* bias; int act; void* aux; const void* dact; const void* resid; int64_t ldr, sR;
+  float alpha; int accumulate; int vec_ok; int vec_c;
+  int splitk; int kchunk; float* slab;  // split-K (TN wgrad): partial slabs [splitk][M][N] f32
+  Drop drop;                            // dropout after the activation, before the residual
+};
+
+template <typename TO>
+__device__ __forceinline__ void epilogue4(const GemmArgs& a, TO* __restrict__ C, const TO* resid,
+                                          TO* aux, const TO* dact, int m, int n, const float* acc,
+                                          int b = 0) {
+  if (m >= a.M || n >= a.N) return;
+  float v[4];
+  bool full = (n + 3 < a.N);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r] = acc[r] * a.alpha;
+    if (a.bias && n + r < a.N) v[r] += a.bias[n + r];
+  }
+  TO* cp = C + (int64_t)m * a.ldc + n;
+  if (dact) {
+    const TO* dp = dact + (int64_t)m * a.ldc + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) v[r] *= act_bwd(a.act, Elem<TO>::ld(dp + r));
+  } else if (a.act) {
+    TO* ap = aux ? aux + (int64_t)m * a.ldc + n : nullptr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r < a.N) {
+        if (ap) Elem<TO>::st(ap + r, v[r]);
+        v[r] = act_fwd(a.act, v[r]);
+      }
+    }
+  }
+  if (a.drop.thr) {
+    const int64_t di = ((int64_t)b * a.M + m) * a.N + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= drop_mul(a.drop, di + r);
+  }
+  if (resid) {
+    const TO* rp = resid + (int64_t)m * a.ldr + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) v[r] += Elem<TO>::ld(rp + r);
+  }
+  if (a.accumulate) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) v[r] += Elem<TO>::ld(cp + r);
+  }
+  if (full && a.vec_c) {
+    if (sizeof(TO) == 2) {
+      u16x4 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      *reinterpret_cast<u16x4*>(cp) = o;
+    } else {
+      f32x4 o = {v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(cp) = o;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < a.N) Elem<TO>::st(cp + r, v[r]);
+  }
+}
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  uint32_t n = bytes <= 0 ? 0u : (bytes >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+
+__device__ __forceinline__ void dma16(rsrc_t r, unsigned short* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMSEQ_LDS void*)lds, 16, voff, 0, 0, 0);
+}
+
+
+}  // namespace mmseq_gemm_detail
+
+// persistent 256 x 256 NT kernel (gemm256.hip); returns false when its preconditions fail
+bool mmseq_gemm256_nt(const mmseq_gemm_detail::GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s,
+                      hipError_t* err);

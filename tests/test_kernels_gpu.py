@@ -417,3 +417,58 @@ def test_vit_im2col_embed_fwd_bwd(dtype):
     _close(dpo, r[0], dtype, scale=2.0)
     for a_, b2 in ((dcls, r[1]), (dpos, r[2]), (dg, r[3]), (db, r[4])):
         _close(a_, b2, torch.float32, scale=10.0 if dtype == torch.float32 else 300.0)
+
+
+@pytest.mark.parametrize("M,Nn,K", [(33000 + 77, 1024, 256), (256 * 3 + 5, 768, 768),
+                                    (2048, 2304, 128), (164160 // 8, 768, 3072)])
+@pytest.mark.parametrize("epi", ["plain", "gelu_aux", "qgelu_aux", "drop_resid", "dgelu", "dqgelu",
+                                 "accum"])
+def test_gemm256_persistent(M, Nn, K, epi):
+    """Persistent 256x256 NT kernel (mode 4 forces it) vs the fp32 reference, and bit-for-bit
+    the same dropout mask as the 128x128 path (mode 2) on the same descriptor."""
+    g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
+    A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(Nn, K, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(Nn, generator=g).to(DEV)
+    resid = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    z_in = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    c0 = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    drop = nat.drop(0.1, 77, 1234) if epi == "drop_resid" else None
+    act = {"gelu_aux": 1, "qgelu_aux": 2, "dgelu": 1, "dqgelu": 2}.get(epi, 0)
+    outs = []
+    for mode in (4, 2):
+        nat.gemm_set_fast(mode)
+        C = c0.clone()
+        aux = torch.empty_like(C) if epi.endswith("aux") else None
+        nat.gemm(A, W, C, M, Nn, K, bias=bias if epi in ("gelu_aux", "qgelu_aux", "drop_resid") else None,
+                 act=act, aux=aux, dact=z_in if epi.startswith("d") and epi != "drop_resid" else None,
+                 resid=resid if epi == "drop_resid" else None, accumulate=epi == "accum", drop=drop)
+        outs.append((C, aux))
+    torch.cuda.synchronize()
+    z = A.float() @ W.float().t()
+    acts = {1: torch.nn.functional.gelu, 2: lambda x: x * torch.sigmoid(1.702 * x)}
+    if epi == "plain":
+        ref = z
+    elif epi.endswith("aux"):
+        z = z + bias
+        ref = acts[act](z)
+        _close(outs[0][1], z, torch.bfloat16, scale=4.0)
+    elif epi == "drop_resid":
+        ref = None
+    elif epi == "accum":
+        ref = z + c0.float()
+    else:
+        zz = z_in.float().requires_grad_(True)
+        gz = torch.autograd.grad(acts[act](zz).sum(), zz)[0]
+        ref = z * gz
+    if ref is not None:
+        _close(outs[0][0], ref, torch.bfloat16, scale=4.0)
+    # identical epilogue math on both paths: at most one bf16 ulp apart (accumulation order)
+    d = (outs[0][0].float() - outs[1][0].float()).abs()
+    tol = 2e-2 * outs[1][0].float().abs() + 2e-2 * math.sqrt(K) / 8
+    assert bool((d <= tol).all()), f"max diff {d.max().item()}"
+    if drop is not None:
+        # the dropped positions (== resid exactly) coincide
+        m4 = outs[0][0] == resid
+        m2 = outs[1][0] == resid
+        assert (m4 != m2).float().mean().item() < 1e-4
