@@ -660,6 +660,31 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
     const bool plain = !bias && !act && !aux_out && !dact_aux && !resid && alpha == 1.0f &&
                        !a.drop.thr &&
                        out_dtype == MMSEQ_F32 && batch == 1 && ldc % 4 == 0 && al16(C);
+    // weight gradients: 256 x 256 TN kernel, K split so that (tiles x splits) fills the CUs
+    if (trans && plain && g_big) {
+      const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+      int S2 = t256 < g_num_cu ? g_num_cu / t256 : 1;
+      if (S2 > K / 1024) S2 = K / 1024 > 0 ? K / 1024 : 1;
+      while (S2 > 1 && (!g_slab || (int64_t)S2 * M * N * 4 > g_slab_bytes)) --S2;
+      GemmArgs t = a;
+      t.splitk = S2;
+      t.kchunk = ((K + S2 - 1) / S2 + 127) / 128 * 128;
+      t.splitk = (K + t.kchunk - 1) / t.kchunk;
+      t.slab = g_slab;
+      hipError_t e2 = hipSuccess;
+      if (t.splitk <= 1) { t.splitk = 1; t.kchunk = K; }
+      if (mmseq_gemm256_tn(t, s, &e2)) {
+        if (e2 == hipSuccess && t.splitk > 1) {
+          int64_t t4 = (int64_t)M * N / 4;
+          unsigned blocks = (unsigned)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
+          hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, M, N, t.splitk,
+                             g_slab, (float*)C, ldc, accumulate);
+          e2 = hipGetLastError();
+        }
+        if (e2 != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm launch: %s", hipGetErrorString(e2));
+        return MMSEQ_OK;
+      }
+    }
     int S = 1;
     if (trans && plain && g_slab && tiles < 512) {
       S = (1024 + tiles - 1) / tiles;

@@ -287,6 +287,159 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Large TN kernel (weight gradients dW[M][N] (+)= sum_k dY[k][M] X[k][N] over the 164k rows):
+// one 256 x 256 output tile x one K-split per 512-thread workgroup, the same 8-phase skeleton as
+// the NT kernel, but the phases split the K-tile by k-half, so a phase reads fragments for every
+// output column: phase 1 A(ks0, i 0-3) + B(ks0, j 0-3), 2 A(ks0, i 4-7), 3 A(ks1, i 0-3) +
+// B(ks1), 4 A(ks1, i 4-7). Half-tiles are whole k-rows (A_ks0 = k 0-31 of the A image, ...), so
+// LDS-DMA pieces are two 512-B rows. Images [64 k][256 m|n], 16-B chunk' = chunk ^ ((k & 7) << 1):
+// the ds_read_b64_tr_b16 fragment reads (8 k-rows x 32 B per 32-lane half) are conflict-free.
+// k order inside a 32-step is permuted identically for both operands (lane group g supplies
+// k {4g..4g+3} U {16+4g..16+4g+3}). Rows past the split's end are zero-filled by the buffer range.
+// Output: fp32, raw partial slab [split][M][N] when split > 1, else C (+)= the tile.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tiles_n, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int G = gridDim.x;
+  const int bid = blockIdx.x;
+  const int item = (G & 7) == 0 ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  const int split = item / ntiles, tile = item - split * ntiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kbeg = split * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+  const int nk = (((kend - kbeg) + 127) >> 7) << 1;  // even number of 64-deep K-tiles
+  const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
+  const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);
+  const rsrc_t ra = make_rsrc(Ab + (int64_t)kbeg * a.lda + m0,
+                              ((int64_t)(kend - kbeg - 1) * a.lda + (a.M - m0)) * 2);
+  const rsrc_t rb = make_rsrc(Bb + (int64_t)kbeg * a.ldb + n0,
+                              ((int64_t)(kend - kbeg - 1) * a.ldb + (a.N - n0)) * 2);
+  const rsrc_t rz = make_rsrc(Ab, 0);
+
+  // DMA piece = 2 k-rows x 512 B; lane -> row (lane >> 5), chunk lane & 31; swizzle term
+  // ((row & 7) << 1) with row & 7 = 2 (q & 3) + (lane >> 5) for wave-instruction q
+  uint32_t offA[4], offB[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int rr = 2 * v + (lane >> 5);
+    const int c = (lane & 31) ^ (rr << 1);
+    offA[v] = (uint32_t)((lane >> 5) * a.lda * 2 + c * 16);
+    offB[v] = (uint32_t)((lane >> 5) * a.ldb * 2 + c * 16);
+  }
+  // half-tile X: 0 = A_ks0, 1 = B_ks0, 2 = A_ks1, 3 = B_ks1 (k-rows 32 (X >> 1) .. +31)
+  auto stage = [&](int kk, int X) {
+    const bool isA = (X & 1) == 0;
+    const rsrc_t r = kk < nk ? (isA ? ra : rb) : rz;
+    const int64_t ld = isA ? a.lda : a.ldb;
+    unsigned short* img = smem + (kk & 1) * (2 * G_LDA_HALF) + (isA ? 0 : G_LDA_HALF);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = wave * 2 + i;
+      const int row = (X >> 1) * 32 + 2 * q;
+      const uint32_t lo = isA ? offA[q & 3] : offB[q & 3];
+      const uint32_t voff = lo + (uint32_t)(((int64_t)kk * 64 + row) * ld * 2);
+      dma16(r, img + row * 256, voff);
+    }
+  };
+
+  // transposed fragment reads: lane (g, ii = 4 q' + p) reads k-row 4g + q' (+16) at column
+  // base + 4p, i.e. chunk 2 (tile) + (p >> 1) XOR-swizzled by ((4g + q') & 7) << 1
+  const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+  const int kr = 4 * g + qq, t8 = kr & 7;
+  int fA[8], fB[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    fA[i] = kr * 256 + (((wr * 16 + 2 * i + (pp >> 1)) ^ (t8 << 1)) << 3) + (pp & 1) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    fB[j] = G_LDA_HALF + kr * 256 + (((wc * 8 + 2 * j + (pp >> 1)) ^ (t8 << 1)) << 3) + (pp & 1) * 4;
+  auto frag = [&](int off) -> bf16x8_t {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(smem + off));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(smem + off + 16 * 256));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8_t fa[8], fb[4];
+
+  stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
+  stage(1, 1); stage(1, 0);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+
+#define TN_PHASE(READS, STAGE, VMWAIT, I0, KS)                                          \
+  READS;                                                                                \
+  STAGE;                                                                                \
+  __builtin_amdgcn_sched_barrier(0);                                                    \
+  if (VMWAIT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                          \
+  __builtin_amdgcn_s_barrier();                                                         \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                    \
+  __builtin_amdgcn_sched_barrier(0);                                                    \
+  __builtin_amdgcn_s_setprio(1);                                                        \
+  _Pragma("unroll") for (int i = I0; i < I0 + 4; ++i)                                   \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                         \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);                                                        \
+  __builtin_amdgcn_sched_barrier(0);                                                    \
+  __builtin_amdgcn_s_barrier();
+
+  for (int s = 0; s < (nk >> 1); ++s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int buf = h * (2 * G_LDA_HALF);
+      // phase 1 (5): ks0, i 0-3
+      TN_PHASE(
+          { _Pragma("unroll") for (int i = 0; i < 4; ++i) fa[i] = frag(buf + fA[i]);
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) fb[j] = frag(buf + fB[j]); },
+          { if (h == 0) stage(2 * s + 1, 3); else stage(2 * s + 2, 3); }, false, 0, 0)
+      // phase 2 (6): ks0, i 4-7
+      TN_PHASE({ _Pragma("unroll") for (int i = 4; i < 8; ++i) fa[i] = frag(buf + fA[i]); },
+               { if (h == 0) stage(2 * s + 1, 2); else stage(2 * s + 2, 2); }, false, 4, 0)
+      // phase 3 (7): ks1, i 0-3
+      TN_PHASE(
+          { _Pragma("unroll") for (int i = 0; i < 4; ++i) fa[i] = frag(buf + 32 * 256 + fA[i]);
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) fb[j] = frag(buf + 32 * 256 + fB[j]); },
+          { if (h == 0) stage(2 * s + 2, 1); else stage(2 * s + 3, 1); }, false, 0, 1)
+      // phase 4 (8): ks1, i 4-7; retire the K-tile read next
+      TN_PHASE({ _Pragma("unroll") for (int i = 4; i < 8; ++i) fa[i] = frag(buf + 32 * 256 + fA[i]); },
+               { if (h == 0) stage(2 * s + 2, 0); else stage(2 * s + 3, 0); }, true, 4, 1)
+    }
+  }
+#undef TN_PHASE
+  if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float* C = a.splitk > 1 ? a.slab + (int64_t)split * a.M * a.N : reinterpret_cast<float*>(a.C);
+  const int64_t ldc = a.splitk > 1 ? a.N : a.ldc;
+  const bool acc_c = a.splitk == 1 && a.accumulate;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wr * 128 + i * 16 + ii;
+      const int n = n0 + wc * 64 + j * 16 + 4 * g;
+      if (m < a.M && n < a.N) {  // N % 8 == 0: n .. n + 3 in range
+        f32x4* cp = reinterpret_cast<f32x4*>(C + (int64_t)m * ldc + n);
+        f32x4 v = acc[i][j];
+        if (acc_c) v += *cp;
+        *cp = v;
+      }
+    }
+}
+
 }  // namespace
 
 bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s, hipError_t* err) {
@@ -312,6 +465,18 @@ bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t 
       break;
     default: return false;
   }
+  *err = hipGetLastError();
+  return true;
+}
+
+bool mmseq_gemm256_tn(const GemmArgs& a, hipStream_t s, hipError_t* err) {
+  auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  if (a.M % 8 != 0 || a.N % 8 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0 || !a16(a.A) || !a16(a.B) ||
+      (a.splitk > 1 && a.kchunk % 128 != 0) || (a.splitk == 1 && (a.ldc % 4 != 0 || !a16(a.C))))
+    return false;
+  const int tn = (a.N + 255) / 256;
+  const int ntiles = ((a.M + 255) / 256) * tn;
+  hipLaunchKernelGGL(gemm256_tn_kernel, dim3(ntiles * a.splitk), dim3(512), 0, s, a, tn, ntiles);
   *err = hipGetLastError();
   return true;
 }
