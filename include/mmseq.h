@@ -38,9 +38,10 @@ typedef enum {
   MMSEQ_ACT_GELU_TANH = 4
 } mmseq_act;
 
-/* Dropout (train mode). Counter-based: keep(idx) = hash(seed, stream, idx) >= p * 2^24, kept
- * values scaled by 1/(1-p); the same (seed, stream) regenerates the mask in the backward, so no
- * mask is ever stored. A NULL pointer or p == 0 means no dropout. */
+/* Dropout (train mode). Counter-based: element idx is dropped iff 16-bit half (idx & 1) of
+ * hash32(key(seed, stream), idx >> 1) < round(p * 2^16) (one 32-bit hash serves an element pair);
+ * kept values are scaled by 1/(1-p). The same (seed, stream) regenerates the mask in the backward,
+ * so no mask is ever stored. A NULL pointer or p == 0 means no dropout. */
 typedef struct {
   float p;
   uint32_t stream;
@@ -104,6 +105,10 @@ mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld
                             int64_t ld_dout, const float* lse, float* delta, void* dqkv,
                             int64_t ld_dqkv, mmseq_dtype dtype, const mmseq_dropout* drop,
                             mmseq_stream stream);
+/* bf16 attention kernel selection: 1 (default) = 128-row workgroups with LDS-DMA double-buffered
+ * K/V (or Q/dO) tiles and the delta = rowsum(dO * O) reduction fused into the dQ kernel;
+ * 0 = 64-row register-staged kernels (cross-check in the tests). fp32 always uses the latter. */
+void mmseq_attn_set_fast(int enable);
 
 /* Small multi-head attention for the BERSON inter-sentence encoder (neural.py:98-235):
  * [B][T][heads*d] separate q/k/v tensors, T <= 64, d <= 128, fp32, key_bias [B][T] or NULL.

@@ -61,6 +61,7 @@ _SIGS = {
                                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                        _dp, _vp]),
     "mmseq_gemm_set_fast": (None, [ctypes.c_int]),
+    "mmseq_attn_set_fast": (None, [ctypes.c_int]),
     "mmseq_gemm_set_workspace": (None, [_vp, _c_i64]),
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
@@ -192,6 +193,12 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
 
 def gemm_set_fast(enable):
     lib().mmseq_gemm_set_fast(int(enable))
+
+
+def attn_set_fast(enable):
+    """bf16 attention kernel selection: 1 = 128-row LDS-DMA pipelined kernels (default), 0 = the
+    64-row kernels (kept as a cross-check in the tests)."""
+    lib().mmseq_attn_set_fast(int(enable))
 
 
 def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse,

@@ -14,13 +14,14 @@
 //      dkdv: per key tile, sweep the queries: S, dP with the key on the lane; dV^T += dO^T P and
 //            dK^T += Q^T dS take P / dS straight from the accumulators.
 //      dq:   per query tile, sweep the keys with the swapped form; dQ^T += K^T dS^T.
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
 
 constexpr int HD = 64;       // head dim
 constexpr int QT = 64;       // rows per workgroup tile
 constexpr float NEG = -1e30f;
+int g_attn_fast = 1;  // bf16: 1 = 128-row DMA-pipelined kernels, 0 = 64-row kernels (tests)
 
 template <typename TI> struct ACfg;
 template <> struct ACfg<unsigned short> { static constexpr int LD = 80, VE = 8; };
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
     if (a.drop.thr) {  // the normaliser l keeps the undropped probabilities (dropout after softmax)
-      const uint64_t rowi = (((uint64_t)p * a.heads + h) * T + (q0 + i)) * T + k0;
+      const uint64_t rowi = (((uint64_t)p * a.heads + h) * T + (q0 + i)) * (uint64_t)((T + 1) & ~1) + k0;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -333,7 +334,8 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         int qi = qs * 16 + 4 * g + r;
         float pv = __expf(s[qs][r] * a.scale + kbias - sL[qi]);
-        const float mul = drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + qb0 + qi) * T + mykey);
+        const float mul = drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + qb0 + qi) *
+                                               (uint64_t)((T + 1) & ~1) + mykey);
         s[qs][r] = pv * mul;
         dp[qs][r] = pv * (dp[qs][r] * mul - sD[qi]);
       }
@@ -459,7 +461,8 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         float pv = __expf(s[kb][r] * a.scale + sBias[kb * 16 + 4 * g + r] - L);
         const float mul =
-            drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + myq) * T + k0 + kb * 16 + 4 * g + r);
+            drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + myq) * (uint64_t)((T + 1) & ~1) + k0 +
+                                 kb * 16 + 4 * g + r);
         dp[kb][r] = pv * (dp[kb][r] * mul - D);
       }
     if constexpr (sizeof(TI) == 2) {
@@ -488,6 +491,507 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnArgs a) {
     for (int d = 0; d < 4; ++d)
 #pragma unroll
       for (int r = 0; r < 4; ++r) Elem<TI>::st(dqp + d * 16 + 4 * g + r, dq[d][r] * a.scale);
+  }
+}
+
+
+// ============================================================================================
+// bf16 fast path (perf mode): 4 waves x 32 rows per workgroup (two 16-row groups per wave share
+// every K/V (or Q/dO) fragment read), 64-row tiles of the swept operand double-buffered in LDS by
+// LDS-DMA (one barrier per tile), exp2-domain softmax with the scale folded into one FMA.
+// LDS images are [64 rows][64] bf16 (128-B rows) with 16-B chunk c of row r stored at
+// c ^ (((r >> 1) & 3) << 1): conflict-free for BOTH the ds_read_b128 row-fragment reads
+// (lane groups of the 16x16x32 operand) and the ds_read_b64_tr_b16 transposed reads, so one image
+// serves S / dP (rows) and dV / dK / dQ (columns). The swizzle is applied to the DMA source.
+// Dropout element index: ((p * heads + h) * T + q) * Tp2 + key, Tp2 = T rounded up to even, so
+// the keys 4g + {0,1} and 4g + {2,3} of a lane share one hash in the forward and dQ kernels.
+// ============================================================================================
+using mmseq_gemm_detail::rsrc_t;
+using mmseq_gemm_detail::make_rsrc;
+using mmseq_gemm_detail::dma16;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr int IMG = 64 * 64;  // elements per [64][64] image
+
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// per-lane LDS-DMA source offset (bytes) of a 1 KB piece (8 rows x 128 B) for row stride ld
+__device__ __forceinline__ uint32_t dma_lane_off(int lane, int64_t ld) {
+  return (uint32_t)((lane >> 3) * ld * 2 + (((lane & 7) ^ (((lane >> 4) & 3) << 1)) << 4));
+}
+// row-fragment offset (elements) for rows rb..rb+15 (rb % 16 == 0): lane (g, i) -> row rb + i,
+// chunk ks * 4 + g
+__device__ __forceinline__ int row_off(int lane, int ks) {
+  const int g = lane >> 4, i = lane & 15;
+  return i * 64 + (((ks * 4 + g) ^ (((i >> 1) & 3) << 1)) << 3);
+}
+// transposed-fragment offset (elements) for output rows d*16..+15 (columns of the image) and
+// k-rows 4g + q (+16 for the high half, + 32 ks): lane (g, i = 4q + p)
+__device__ __forceinline__ int tr_off(int lane, int d) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int v = (2 * g + (q >> 1)) & 3;
+  return (4 * g + q) * 64 + ((2 * (d ^ v) + (pp >> 1)) << 3) + (pp & 1) * 4;
+}
+__device__ __forceinline__ bf16x8_t lds_row(const unsigned short* img, int off) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(img + off));
+}
+__device__ __forceinline__ bf16x8_t lds_tr(const unsigned short* img, int off) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(img + off));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MMSEQ_LDS s16x4*)(img + off + 16 * 64));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+__device__ __forceinline__ f32x4 mma(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ rsrc_t head_rsrc(const void* base, int64_t row0, int64_t ld, int64_t col,
+                                            int T) {
+  const unsigned short* b = reinterpret_cast<const unsigned short*>(base) + row0 * ld + col;
+  return make_rsrc(b, ((int64_t)(T - 1) * ld + 64) * 2);
+}
+
+// ---- forward ---------------------------------------------------------------------------------
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
+  float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int h = blockIdx.y, p = blockIdx.z, T = a.T;
+  const int nkt = (T + 63) >> 6;
+  const int qw = blockIdx.x * 128 + wave * 32;
+  const bool active = qw < T;
+  const int64_t ld = a.ld_qkv;
+  const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
+  const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
+  const uint32_t loff = dma_lane_off(lane, ld);
+  auto stage = [&](int t) {
+    unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pc = wave * 2 + e;
+      const uint32_t vo = loff + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2);
+      dma16(rk, kimg + pc * 512, vo);
+      dma16(rv, kimg + IMG + pc * 512, vo);
+    }
+  };
+  stage(0);
+  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+  for (int k = tid; k < nkt * 64; k += 256)
+    sBias[k] = k < T ? (kbias ? kbias[k] * LOG2E : 0.f) : -1e30f;
+  const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
+                             a.q_off + h * 64;
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[grp][ks] = glob_row_frag(Qb, ld, qw + grp * 16 + i, T, ks, lane);
+
+  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
+  const float c = a.scale * LOG2E;
+  const int Tp2 = (T + 1) & ~1;
+  uint64_t drow[2];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+    drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp2;
+
+  f32x4 o[2][4];
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < nkt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile t landed everywhere; buffer (t + 1) & 1 no longer read
+    if (t + 1 < nkt) stage(t + 1);
+    if (!active) continue;
+    const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+    const unsigned short* vimg = kimg + IMG;
+    f32x4 s[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16x8_t k0 = lds_row(kimg, kb * 1024 + ro0), k1 = lds_row(kimg, kb * 1024 + ro1);
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        s[grp][kb] = mma(k0, qf[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
+        s[grp][kb] = mma(k1, qf[grp][1], s[grp][kb]);
+      }
+    }
+    f32x4 bias[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+      bias[kb] = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 16 + 4 * g);
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int grp = 0; grp < 2; ++grp) {
+      float mx = -1e30f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = fmaf(s[grp][kb][r], c, bias[kb][r]);
+          s[grp][kb][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[grp], mx);
+      const float alpha = ex2(m[grp] - mn);
+      m[grp] = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = ex2(s[grp][kb][r] - mn);
+          s[grp][kb][r] = e;
+          rs += e;
+        }
+      l[grp] = fmaf(l[grp], alpha, rs);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[grp][d] *= alpha;
+      if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          float dm[4];
+          drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[grp][kb][r] *= dm[r];
+        }
+      }
+      pf[grp][0] = pack_pair(s[grp][0], s[grp][1]);
+      pf[grp][1] = pack_pair(s[grp][2], s[grp][3]);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const bf16x8_t v0 = lds_tr(vimg, to[d]), v1 = lds_tr(vimg, 32 * 64 + to[d]);
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        o[grp][d] = mma(v0, pf[grp][0], o[grp][d]);
+        o[grp][d] = mma(v1, pf[grp][1], o[grp][d]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!active) return;
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    float lt = l[grp];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int q = qw + grp * 16 + i;
+    if (q < T) {
+      const float inv = 1.0f / lt;
+      unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
+                           h * 64 + 4 * g;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(op + d * 16, o[grp][d] * inv);
+      if (g == 0) a.lse[((int64_t)p * a.heads + h) * T + q] = (m[grp] + __builtin_amdgcn_logf(lt)) * LN2;
+    }
+  }
+}
+
+// ---- backward: dQ (per 128-query block, keys swept), also writes delta = rowsum(dO * O) --------
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+  float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int h = blockIdx.y, p = blockIdx.z, T = a.T;
+  const int nkt = (T + 63) >> 6;
+  const int qw = blockIdx.x * 128 + wave * 32;
+  const bool active = qw < T;
+  const int64_t ld = a.ld_qkv;
+  const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
+  const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
+  const uint32_t loff = dma_lane_off(lane, ld);
+  auto stage = [&](int t) {
+    unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pc = wave * 2 + e;
+      const uint32_t vo = loff + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2);
+      dma16(rk, kimg + pc * 512, vo);
+      dma16(rv, kimg + IMG + pc * 512, vo);
+    }
+  };
+  stage(0);
+  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+  for (int k = tid; k < nkt * 64; k += 256)
+    sBias[k] = k < T ? (kbias ? kbias[k] * LOG2E : 0.f) : -1e30f;
+  const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
+                             a.q_off + h * 64;
+  const unsigned short* dOb = reinterpret_cast<const unsigned short*>(a.dout) +
+                              (int64_t)p * T * a.ld_dout + h * 64;
+  const unsigned short* Ob = reinterpret_cast<const unsigned short*>(a.out) +
+                             (int64_t)p * T * a.ld_out + h * 64;
+  bf16x8_t qf[2][2], of[2][2];
+  float L2[2], Dd[2];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int q = qw + grp * 16 + i;
+    float dot = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[grp][ks] = glob_row_frag(Qb, ld, q, T, ks, lane);
+      of[grp][ks] = glob_row_frag(dOb, a.ld_dout, q, T, ks, lane);
+      const bf16x8_t ov = glob_row_frag(Ob, a.ld_out, q, T, ks, lane);
+      const u16x8 x = __builtin_bit_cast(u16x8, of[grp][ks]), y = __builtin_bit_cast(u16x8, ov);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot = fmaf(bf2f(x[e]), bf2f(y[e]), dot);
+    }
+    dot += __shfl_xor(dot, 16, 64);
+    dot += __shfl_xor(dot, 32, 64);
+    Dd[grp] = dot;
+    const int64_t ri = ((int64_t)p * a.heads + h) * T + q;
+    L2[grp] = q < T ? a.lse[ri] * LOG2E : 1e30f;
+    if (q < T && g == 0) a.delta[ri] = dot;
+  }
+  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
+  const float c = a.scale * LOG2E;
+  const int Tp2 = (T + 1) & ~1;
+  uint64_t drow[2];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+    drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp2;
+  f32x4 dq[2][4];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dq[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < nkt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nkt) stage(t + 1);
+    if (!active) continue;
+    const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+    const unsigned short* vimg = kimg + IMG;
+    f32x4 s[2][4], dp[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16x8_t k0 = lds_row(kimg, kb * 1024 + ro0), k1 = lds_row(kimg, kb * 1024 + ro1);
+      const bf16x8_t v0 = lds_row(vimg, kb * 1024 + ro0), v1 = lds_row(vimg, kb * 1024 + ro1);
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        s[grp][kb] = mma(k0, qf[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
+        s[grp][kb] = mma(k1, qf[grp][1], s[grp][kb]);
+        dp[grp][kb] = mma(v0, of[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
+        dp[grp][kb] = mma(v1, of[grp][1], dp[grp][kb]);
+      }
+    }
+    f32x4 bias[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+      bias[kb] = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 16 + 4 * g);
+    bf16x8_t dsf[2][2];
+#pragma unroll
+    for (int grp = 0; grp < 2; ++grp) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        float dm[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = ex2(fmaf(s[grp][kb][r], c, bias[kb][r]) - L2[grp]);
+          dp[grp][kb][r] = pv * fmaf(dp[grp][kb][r], dm[r], -Dd[grp]);
+        }
+      }
+      dsf[grp][0] = pack_pair(dp[grp][0], dp[grp][1]);
+      dsf[grp][1] = pack_pair(dp[grp][2], dp[grp][3]);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const bf16x8_t k0 = lds_tr(kimg, to[d]), k1 = lds_tr(kimg, 32 * 64 + to[d]);
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        dq[grp][d] = mma(k0, dsf[grp][0], dq[grp][d]);
+        dq[grp][d] = mma(k1, dsf[grp][1], dq[grp][d]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!active) return;
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int q = qw + grp * 16 + i;
+    if (q < T) {
+      unsigned short* dqp = reinterpret_cast<unsigned short*>(a.dqkv) +
+                            ((int64_t)p * T + q) * a.ld_dqkv + a.q_off + h * 64 + 4 * g;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(dqp + d * 16, dq[grp][d] * a.scale);
+    }
+  }
+}
+
+// ---- backward: dK, dV (per 128-key block, queries swept; key on the MFMA lane) ----------------
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (Q, dO) + lse, D
+  const int T = a.T;
+  const int nqt = (T + 63) >> 6;
+  float* sL = reinterpret_cast<float*>(smem + 4 * IMG);
+  float* sD = sL + nqt * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int h = blockIdx.y, p = blockIdx.z;
+  const int kw = blockIdx.x * 128 + wave * 32;
+  const bool active = kw < T;
+  const int64_t ld = a.ld_qkv;
+  const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
+  const rsrc_t ro = head_rsrc(a.dout, (int64_t)p * T, a.ld_dout, h * 64, T);
+  const uint32_t loffq = dma_lane_off(lane, ld), loffo = dma_lane_off(lane, a.ld_dout);
+  auto stage = [&](int t) {
+    unsigned short* qimg = smem + (t & 1) * 2 * IMG;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pc = wave * 2 + e;
+      dma16(rq, qimg + pc * 512, loffq + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2));
+      dma16(ro, qimg + IMG + pc * 512, loffo + (uint32_t)((int64_t)(t * 64 + pc * 8) * a.ld_dout * 2));
+    }
+  };
+  stage(0);
+  const int64_t rb = ((int64_t)p * a.heads + h) * T;
+  for (int q = tid; q < nqt * 64; q += 256) {
+    sL[q] = q < T ? a.lse[rb + q] * LOG2E : 1e30f;  // exp2(x - 1e30) = 0 for padded queries
+    sD[q] = q < T ? a.delta[rb + q] : 0.f;
+  }
+  const unsigned short* Kb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
+                             a.k_off + h * 64;
+  const unsigned short* Vb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
+                             a.v_off + h * 64;
+  bf16x8_t kf[2][2], vf[2][2];
+  float kb2[2];
+  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int key = kw + grp * 16 + i;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[grp][ks] = glob_row_frag(Kb, ld, key, T, ks, lane);
+      vf[grp][ks] = glob_row_frag(Vb, ld, key, T, ks, lane);
+    }
+    kb2[grp] = key < T ? (kbias ? kbias[key] * LOG2E : 0.f) : -1e30f;
+  }
+  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
+  const float c = a.scale * LOG2E;
+  const int Tp2 = (T + 1) & ~1;
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dk[grp][d] = dv[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < nqt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nqt) stage(t + 1);
+    if (!active) continue;
+    const unsigned short* qimg = smem + (t & 1) * 2 * IMG;
+    const unsigned short* oimg = qimg + IMG;
+    // dropout keep-bits of this lane's 32 (q, key) elements, bit grp*16 + qs*4 + r, computed
+    // before the MFMAs (few live registers); (q, key) -> index (rb + q) * Tp2 + key
+    uint32_t keep = 0xFFFFFFFFu;
+    if (DROP) {
+      keep = 0;
+      const uint64_t dbase = (uint64_t)(rb + t * 64 + 4 * g) * (uint64_t)Tp2 + kw + i;
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint64_t idx = dbase + (uint64_t)((qs * 16 + r) * Tp2 + grp * 16);
+            const uint32_t h = drop_hash(a.drop, idx >> 1);
+            const uint32_t u = (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+            keep |= (u >= a.drop.thr ? 1u : 0u) << (grp * 16 + qs * 4 + r);
+          }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the hashing ahead of the MFMAs (register pressure)
+    // two halves of the 64-query tile (k-step ks of the dV / dK products = queries 32ks..+31):
+    // S[q][key], dP[q][key] with the key on the lane (q = qs*16 + 4g + r, key = grp*16 + i), then
+    // P / dS, then dV^T[d][key] += dO^T[d][q] P[q][key] and dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f32x4 s[2][2], dp[2][2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int qs = 2 * ks + h2;
+        const bf16x8_t q0 = lds_row(qimg, qs * 1024 + ro0), q1 = lds_row(qimg, qs * 1024 + ro1);
+        const bf16x8_t o0 = lds_row(oimg, qs * 1024 + ro0), o1 = lds_row(oimg, qs * 1024 + ro1);
+#pragma unroll
+        for (int grp = 0; grp < 2; ++grp) {
+          s[grp][h2] = mma(q0, kf[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
+          s[grp][h2] = mma(q1, kf[grp][1], s[grp][h2]);
+          dp[grp][h2] = mma(o0, vf[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
+          dp[grp][h2] = mma(o1, vf[grp][1], dp[grp][h2]);
+        }
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int qs = 2 * ks + h2;
+        const f32x4 Lq = *reinterpret_cast<const f32x4*>(sL + t * 64 + qs * 16 + 4 * g);
+        const f32x4 Dq = *reinterpret_cast<const f32x4*>(sD + t * 64 + qs * 16 + 4 * g);
+#pragma unroll
+        for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = ex2(fmaf(s[grp][h2][r], c, kb2[grp]) - Lq[r]);
+            float mk = 1.f;
+            if (DROP) mk = ((keep >> (grp * 16 + qs * 4 + r)) & 1u) ? a.drop.scale : 0.f;
+            s[grp][h2][r] = pv * mk;
+            dp[grp][h2][r] = pv * fmaf(dp[grp][h2][r], mk, -Dq[r]);
+          }
+      }
+      bf16x8_t pf[2], dsf[2];
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        pf[grp] = pack_pair(s[grp][0], s[grp][1]);
+        dsf[grp] = pack_pair(dp[grp][0], dp[grp][1]);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8_t ov = lds_tr(oimg, ks * 32 * 64 + to[d]);
+        const bf16x8_t qv = lds_tr(qimg, ks * 32 * 64 + to[d]);
+#pragma unroll
+        for (int grp = 0; grp < 2; ++grp) {
+          dv[grp][d] = mma(ov, pf[grp], dv[grp][d]);
+          dk[grp][d] = mma(qv, dsf[grp], dk[grp][d]);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!active) return;
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int key = kw + grp * 16 + i;
+    if (key < T) {
+      unsigned short* row = reinterpret_cast<unsigned short*>(a.dqkv) + ((int64_t)p * T + key) * a.ld_dqkv;
+      unsigned short* dkp = row + a.k_off + h * 64 + 4 * g;
+      unsigned short* dvp = row + a.v_off + h * 64 + 4 * g;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        Vec4<unsigned short>::st(dkp + d * 16, dk[grp][d] * a.scale);
+        Vec4<unsigned short>::st(dvp + d * 16, dv[grp][d]);
+      }
+    }
   }
 }
 
@@ -523,7 +1027,15 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   a.drop = make_drop(drop);
   dim3 grid((T + QT - 1) / QT, heads, P);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (dtype == MMSEQ_BF16)
+  if (dtype == MMSEQ_BF16 && g_attn_fast) {
+    MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
+    const dim3 gq((T + 127) / 128, heads, P);
+    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4;
+    if (a.drop.thr)
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel<true>, gq, dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel<false>, gq, dim3(256), lds, s, a);
+  } else if (dtype == MMSEQ_BF16)
     hipLaunchKernelGGL(attn_fwd_kernel<unsigned short>, grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, s, a);
@@ -554,7 +1066,19 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   const int64_t rows = (int64_t)P * T;
   dim3 gd((unsigned)((rows + 3) / 4));
   dim3 grid((T + QT - 1) / QT, heads, P);
-  if (dtype == MMSEQ_BF16) {
+  if (dtype == MMSEQ_BF16 && g_attn_fast) {
+    MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0 && aligned16(dqkv) && ld_dqkv % 8 == 0,
+                  "attn_bwd: out / dqkv must be 16-byte aligned rows");
+    const dim3 gq((T + 127) / 128, heads, P);
+    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2;
+    if (a.drop.thr) {
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<true>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<true>, gq, dim3(256), lds, s, a);
+    } else {
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<false>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<false>, gq, dim3(256), lds, s, a);
+    }
+  } else if (dtype == MMSEQ_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<unsigned short>, gd, dim3(256), 0, s, a);
     hipLaunchKernelGGL(attn_dkdv_kernel<unsigned short>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(attn_dq_kernel<unsigned short>, grid, dim3(256), 0, s, a);
@@ -565,3 +1089,5 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   }
   return mmseq_check_launch("attn_bwd");
 }
+
+extern "C" void mmseq_attn_set_fast(int enable) { g_attn_fast = enable != 0; }

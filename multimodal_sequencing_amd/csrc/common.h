@@ -102,36 +102,105 @@ __device__ __forceinline__ float act_bwd(int act, float x) {
   }
 }
 
+// --- fast activations for the bf16 GEMM epilogues (no divergent libm branches) ---------------
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16 resolution); the
+// exp(-x^2) term is shared with the GELU derivative's pdf.
+__device__ __forceinline__ void erf_and_gauss(float x, float& erf_x, float& e) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  poly *= t;
+  e = __expf(-ax * ax);
+  erf_x = copysignf(fmaf(-poly, e, 1.0f), x);
+}
+__device__ __forceinline__ float act_fwd_fast(int act, float x) {
+  if (act == MMSEQ_ACT_GELU_ERF) {
+    float er, e;
+    erf_and_gauss(x * 0.70710678118654752f, er, e);
+    return 0.5f * x * (1.0f + er);
+  }
+  if (act == MMSEQ_ACT_QUICKGELU) return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+  return act_fwd(act, x);
+}
+__device__ __forceinline__ float act_bwd_fast(int act, float x) {
+  if (act == MMSEQ_ACT_GELU_ERF) {
+    float er, e;  // e = exp(-x^2 / 2)
+    erf_and_gauss(x * 0.70710678118654752f, er, e);
+    return fmaf(0.39894228040143268f * x, e, 0.5f * (1.0f + er));
+  }
+  if (act == MMSEQ_ACT_QUICKGELU) {
+    const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+    return s + 1.702f * x * s * (1.0f - s);
+  }
+  return act_bwd(act, x);
+}
+
 // --- dropout: counter-based mask (no stored masks; fwd and bwd regenerate the same bits) ---
+// One 32-bit hash per element PAIR (idx >> 1); element idx uses 16-bit half (idx & 1) against a
+// 16-bit threshold round(p * 2^16). The per-call key is derived on the host from (seed, stream)
+// by splitmix64, so streams and seeds are independent; the per-pair mix is Wellons' lowbias32.
 struct Drop {
-  uint32_t thr;     // drop iff (hash >> 8) < thr   (thr = p * 2^24); thr == 0 -> disabled
-  uint32_t stream;
-  uint64_t seed;
+  uint32_t thr;     // drop iff half < thr; thr == 0 -> disabled
+  uint32_t k0, k1;  // per-call key
   float scale;      // 1 / (1 - p)
 };
+__host__ inline uint64_t drop_splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
 __host__ inline Drop make_drop(const mmseq_dropout* d) {
   Drop r;
-  r.thr = 0; r.stream = 0; r.seed = 0; r.scale = 1.f;
+  r.thr = 0; r.k0 = 0; r.k1 = 0; r.scale = 1.f;
   if (d && d->p > 0.f) {
-    r.thr = (uint32_t)(d->p * 16777216.0f);
-    r.stream = d->stream;
-    r.seed = d->seed;
+    uint32_t t = (uint32_t)(d->p * 65536.0f + 0.5f);
+    r.thr = t < 1u ? 1u : t;
+    const uint64_t key = drop_splitmix64(d->seed ^ drop_splitmix64(0x5bd1e995ull + d->stream));
+    r.k0 = (uint32_t)key;
+    r.k1 = (uint32_t)(key >> 32) | 1u;
     r.scale = 1.0f / (1.0f - d->p);
   }
   return r;
 }
-__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t idx) {
-  uint32_t h = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x9e3779b1u) ^ (uint32_t)d.seed ^
-               (d.stream * 0x85ebca77u);
-  h *= 0xcc9e2d51u;
-  h ^= (uint32_t)(d.seed >> 32) + 0x27d4eb2fu;
-  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;  // fmix32
-  return h;
+__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t pair) {
+  uint32_t x = ((uint32_t)pair ^ d.k0) + (uint32_t)(pair >> 32) * d.k1;
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float drop_sel(const Drop& d, uint32_t h, int hi) {
+  const uint32_t u = hi ? (h >> 16) : (h & 0xFFFFu);
+  return u < d.thr ? 0.f : d.scale;
 }
 // multiplier for element idx: 0 (dropped) or 1/(1-p); 1 when disabled
 __device__ __forceinline__ float drop_mul(const Drop& d, uint64_t idx) {
   if (d.thr == 0) return 1.f;
-  return (drop_hash(d, idx) >> 8) < d.thr ? 0.f : d.scale;
+  return drop_sel(d, drop_hash(d, idx >> 1), (int)(idx & 1));
+}
+// multipliers for elements idx .. idx + 2n - 1 with idx EVEN (one hash per pair)
+template <int NPAIR>
+__device__ __forceinline__ void drop_mul_pairs(const Drop& d, uint64_t idx, float* m) {
+  const uint64_t j = idx >> 1;
+#pragma unroll
+  for (int q = 0; q < NPAIR; ++q) {
+    const uint32_t h = drop_hash(d, j + q);
+    m[2 * q] = drop_sel(d, h, 0);
+    m[2 * q + 1] = drop_sel(d, h, 1);
+  }
+}
+// multipliers for the 4 elements idx .. idx + 3 (pair-shared hashes when idx is even)
+__device__ __forceinline__ void drop_mul4(const Drop& d, uint64_t idx, float* m) {
+  if (d.thr == 0) {
+    m[0] = m[1] = m[2] = m[3] = 1.f;
+  } else if ((idx & 1) == 0) {
+    drop_mul_pairs<2>(d, idx, m);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = drop_mul(d, idx + e);
+  }
 }
 
 // status plumbing shared by the ABI wrappers

@@ -30,24 +30,32 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
 #pragma unroll
   for (int r = 0; r < 4; ++r) { v[r] = lo[r] * a.alpha; v[4 + r] = hi[r] * a.alpha; }
   if (a.bias) {
+    if ((((uintptr_t)a.bias) & 15) == 0) {  // wave-uniform: two 16-byte loads
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] += a.bias[n + r];
+      for (int r = 0; r < 4; ++r) { v[r] += b0[r]; v[4 + r] += b1[r]; }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] += a.bias[n + r];
+    }
   }
   const int64_t off = (int64_t)m * a.ldc + n;
   if (BWD) {
     float d[8];
     ld8(reinterpret_cast<const us*>(a.dact) + off, d);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] *= act_bwd(ACT, d[r]);
+    for (int r = 0; r < 8; ++r) v[r] *= act_bwd_fast(ACT, d[r]);
   } else if (ACT) {
     if (a.aux) st8(reinterpret_cast<us*>(a.aux) + off, v);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = act_fwd(ACT, v[r]);
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
   }
-  if (a.drop.thr) {
-    const int64_t di = (int64_t)m * a.N + n;
+  if (a.drop.thr) {  // m * N + n is even (N % 8 == 0, n % 8 == 0): one hash per pair
+    float dm[8];
+    drop_mul_pairs<4>(a.drop, (uint64_t)m * a.N + n, dm);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] *= drop_mul(a.drop, di + r);
+    for (int r = 0; r < 8; ++r) v[r] *= dm[r];
   }
   if (a.resid) {
     float t[8];

@@ -78,9 +78,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
     const int c = j * 256 + lane * 4;
     if (c >= cols) continue;
     f32x4 g = ldp(gamma, c, cols), b = ldp(beta, c, cols), o;
+    float dm[4];
+    drop_mul4(dy_, (uint64_t)r * cols + c, dm);
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      o[e] = ((v[j][e] - mu) * rs * g[e] + b[e]) * drop_mul(dy_, (uint64_t)r * cols + c + e);
+    for (int e = 0; e < 4; ++e) o[e] = ((v[j][e] - mu) * rs * g[e] + b[e]) * dm[e];
     st4<TY, VEC>(yr, c, cols, o);
   }
   if (lane == 0) {
@@ -121,8 +122,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
       const int c = j * 256 + lane * 4;
       f32x4 xv = ld4<T, VEC>(xr, c, cols), d = ld4<T, VEC>(dyr, c, cols);
       if (din.thr) {
+        float dm[4];
+        drop_mul4(din, (uint64_t)r * cols + c, dm);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[e] *= drop_mul(din, (uint64_t)r * cols + c + e);
+        for (int e = 0; e < 4; ++e) d[e] *= dm[e];
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -149,8 +152,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
       for (int e = 0; e < 4; ++e) o[e] = rs * (gdy[j][e] - s1 - xh[j][e] * s2);
       if (dxd) {
         f32x4 od;
+        float dm[4];
+        drop_mul4(dout, (uint64_t)r * cols + c, dm);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) od[e] = o[e] * drop_mul(dout, (uint64_t)r * cols + c + e);
+        for (int e = 0; e < 4; ++e) od[e] = o[e] * dm[e];
         st4<T, VEC>(dxd + row_off(dxl, r), c, cols, od);
       }
       if (drr) {

@@ -145,8 +145,11 @@ def _attn_ref(qkv, P, T, heads, bias, scale):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("P,T,heads,masked", [(2, 64, 1, False), (3, 129, 2, True), (2, 33, 2, True),
-                                              (1, 513, 12, True), (2, 393, 2, False)])
-def test_attention_fwd_bwd(dtype, P, T, heads, masked):
+                                              (1, 513, 12, True), (2, 393, 2, False), (1, 1, 1, False),
+                                              (2, 127, 1, True)])
+@pytest.mark.parametrize("fast", [1, 0])
+def test_attention_fwd_bwd(dtype, P, T, heads, masked, fast):
+    nat.attn_set_fast(fast)
     g = torch.Generator(device="cpu").manual_seed(P * T + heads)
     H = heads * 64
     qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, dtype)
@@ -169,6 +172,7 @@ def test_attention_fwd_bwd(dtype, P, T, heads, masked):
                dqkv, 3 * H)
     (ref_g,) = torch.autograd.grad(ref, qf, dout.float())
     _close(dqkv, ref_g, dtype, scale=2.0)
+    nat.attn_set_fast(1)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
