@@ -139,7 +139,11 @@ __global__ __launch_bounds__(NT_THREADS) void gemm_kernel(GemmArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, b = blockIdx.z;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  // split-K (plain fp32 TN / NT with few tiles): blockIdx.z is the K slice, output a raw slab
+  const int split = a.splitk > 1 ? blockIdx.z : 0, b = a.splitk > 1 ? 0 : blockIdx.z;
+  const int kbeg = split * a.kchunk;
+  const int kend = a.splitk > 1 ? min(a.K, kbeg + a.kchunk) : a.K;
   const TI* A = reinterpret_cast<const TI*>(a.A) + (int64_t)b * a.sA;
   const TI* B = reinterpret_cast<const TI*>(a.B) + (int64_t)b * a.sB;
   const bool vec = a.vec_ok;
@@ -151,11 +155,11 @@ __global__ __launch_bounds__(NT_THREADS) void gemm_kernel(GemmArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   V ra[Tl::NCHUNK], rb[Tl::NCHUNK];
-  const int nk = (a.K + BK - 1) / BK;
+  const int nk = (kend - kbeg + BK - 1) / BK;
 #pragma unroll
   for (int c = 0; c < Tl::NCHUNK; ++c) {
-    ra[c] = load_chunk<TI, TRANS>(A, a.lda, m0, 0, c, tid, a.M, a.K, vec);
-    rb[c] = load_chunk<TI, TRANS>(B, a.ldb, n0, 0, c, tid, a.N, a.K, vec);
+    ra[c] = load_chunk<TI, TRANS>(A, a.lda, m0, kbeg, c, tid, a.M, kend, vec);
+    rb[c] = load_chunk<TI, TRANS>(B, a.ldb, n0, kbeg, c, tid, a.N, kend, vec);
   }
 #pragma unroll
   for (int c = 0; c < Tl::NCHUNK; ++c) {
@@ -169,8 +173,8 @@ __global__ __launch_bounds__(NT_THREADS) void gemm_kernel(GemmArgs a) {
     if (more) {
 #pragma unroll
       for (int c = 0; c < Tl::NCHUNK; ++c) {
-        ra[c] = load_chunk<TI, TRANS>(A, a.lda, m0, (kt + 1) * BK, c, tid, a.M, a.K, vec);
-        rb[c] = load_chunk<TI, TRANS>(B, a.ldb, n0, (kt + 1) * BK, c, tid, a.N, a.K, vec);
+        ra[c] = load_chunk<TI, TRANS>(A, a.lda, m0, kbeg + (kt + 1) * BK, c, tid, a.M, kend, vec);
+        rb[c] = load_chunk<TI, TRANS>(B, a.ldb, n0, kbeg + (kt + 1) * BK, c, tid, a.N, kend, vec);
       }
     }
     if constexpr (sizeof(TI) == 2) {
@@ -226,11 +230,27 @@ __global__ __launch_bounds__(NT_THREADS) void gemm_kernel(GemmArgs a) {
     }
   }
 
+  const int g = lane >> 4, ii = lane & 15;
+  if (a.splitk > 1) {  // raw fp32 partial slab [split][M][N], reduced by splitk_reduce
+    float* slab = a.slab + (int64_t)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wr * 64 + i * 16 + ii;
+        const int n = n0 + wc * 64 + j * 16 + 4 * g;
+        if (m < a.M) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < a.N) slab[(int64_t)m * a.N + n + r] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   TO* C = reinterpret_cast<TO*>(a.C) + (int64_t)b * a.sC;
   const TO* resid = a.resid ? reinterpret_cast<const TO*>(a.resid) + (int64_t)b * a.sR : nullptr;
   TO* aux = a.aux ? reinterpret_cast<TO*>(a.aux) + (int64_t)b * a.sC : nullptr;
   const TO* dact = a.dact ? reinterpret_cast<const TO*>(a.dact) + (int64_t)b * a.sC : nullptr;
-  const int g = lane >> 4, ii = lane & 15;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -551,6 +571,21 @@ __global__ __launch_bounds__(256, 2) void gemm_ring_kernel(GemmArgs a, int tiles
 }
 
 // C[m][n] (+)= sum_s slab[s][m][n], fixed order (bitwise reproducible)
+// C[m][n] (+)= sum_s slab[s][m][n] for any N (element-wise; the generic split-K path)
+__global__ __launch_bounds__(256) void splitk_reduce1_kernel(int M, int N, int S, const float* __restrict__ slab,
+                                                             float* __restrict__ C, int64_t ldc,
+                                                             int accumulate) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int m = e / N, n = e % N;
+    float v = slab[e];
+    for (int s = 1; s < S; ++s) v += slab[(int64_t)s * total + e];
+    float* cp = C + (int64_t)m * ldc + n;
+    if (accumulate) v += *cp;
+    *cp = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S, const float* __restrict__ slab,
                                                             float* __restrict__ C, int64_t ldc,
                                                             int accumulate) {
@@ -709,6 +744,37 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
     } else {
       e = out_dtype == MMSEQ_BF16 ? launch_fast<unsigned short>(trans, a, batch, s)
                                   : launch_fast<float>(trans, a, batch, s);
+    }
+  } else if (in_dtype == MMSEQ_F32 && out_dtype == MMSEQ_F32 && batch == 1 && g_slab && !bias &&
+             !act && !aux_out && !dact_aux && !resid && alpha == 1.0f && !a.drop.thr &&
+             ((M + 127) / 128) * ((N + 127) / 128) < 128 && K >= 2048) {
+    // skinny fp32 GEMMs with a long K (head weight gradients over all tokens): split K over
+    // the CUs, fp32 partial slabs, fixed-order reduction (bitwise reproducible)
+    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    int S = (g_num_cu + tiles - 1) / tiles;
+    if (S > K / 512) S = K / 512;
+    while (S > 1 && (int64_t)S * M * N * 4 > g_slab_bytes) --S;
+    a.splitk = S;
+    a.kchunk = ((K + S - 1) / S + 31) / 32 * 32;
+    a.splitk = (K + a.kchunk - 1) / a.kchunk;
+    a.slab = g_slab;
+    if (a.splitk > 1) {
+      dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, a.splitk);
+      if (trans)
+        hipLaunchKernelGGL((gemm_kernel<float, float, true>), grid, dim3(NT_THREADS), 0, s, a);
+      else
+        hipLaunchKernelGGL((gemm_kernel<float, float, false>), grid, dim3(NT_THREADS), 0, s, a);
+      e = hipGetLastError();
+      if (e == hipSuccess) {
+        const int64_t tot = (int64_t)M * N;
+        const unsigned blocks = (unsigned)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096);
+        hipLaunchKernelGGL(splitk_reduce1_kernel, dim3(blocks), dim3(256), 0, s, M, N, a.splitk,
+                           g_slab, (float*)C, ldc, accumulate);
+        e = hipGetLastError();
+      }
+    } else {
+      a.splitk = 1; a.kchunk = K; a.slab = nullptr;
+      e = launch<float, float>(trans, a, batch, s);
     }
   } else if (in_dtype == MMSEQ_BF16 && out_dtype == MMSEQ_BF16)
     e = launch<unsigned short, unsigned short>(trans, a, batch, s);

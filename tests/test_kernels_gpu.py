@@ -476,3 +476,27 @@ def test_gemm256_persistent(M, Nn, K, epi):
         m4 = outs[0][0] == resid
         m2 = outs[1][0] == resid
         assert (m4 != m2).float().mean().item() < 1e-4
+
+
+@pytest.mark.parametrize("trans,M,N,K", [(1, 1, 768, 38400), (1, 768, 768, 38400), (1, 130, 96, 5000),
+                                         (0, 100, 768, 4096), (0, 3, 5, 2049)])
+def test_gemm_fp32_splitk(trans, M, N, K):
+    """Skinny fp32 GEMMs with a long K take the split-K generic path (slabs + ordered reduce)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    if trans:
+        A = torch.randn(K, M, generator=g).to(DEV)
+        B = torch.randn(K, N, generator=g).to(DEV)
+        ref0 = A.t() @ B
+    else:
+        A = torch.randn(M, K, generator=g).to(DEV)
+        B = torch.randn(N, K, generator=g).to(DEV)
+        ref0 = A @ B.t()
+    C0 = torch.randn(M, N, generator=g).to(DEV)
+    C = C0.clone()
+    nat.gemm(A, B, C, M, N, K, trans=trans, accumulate=True)
+    C2 = C0.clone()
+    nat.gemm(A, B, C2, M, N, K, trans=trans, accumulate=True)
+    assert torch.equal(C, C2)  # fixed-order reduction: bitwise reproducible
+    ref = C0.double() + (A.double().t() @ B.double() if trans else A.double() @ B.double().t())
+    err = (C.double() - ref).abs().max().item()
+    assert err <= 1e-5 * math.sqrt(K) * (1 + ref.abs().max().item()) / 8, err
