@@ -12,8 +12,11 @@ namespace {
 constexpr int MAXJ = 4;   // 4 x 256 columns
 constexpr int RPB = 128;  // rows per workgroup in bwd (dgamma/dbeta partial granularity)
 
+// 32-bit division (rows < 2^31): a 64-bit divide is a ~100-instruction branchy subroutine
 __device__ __forceinline__ int64_t row_off(const mmseq_rows& l, int64_t r) {
-  return (r / l.rpb) * l.bstride + (r % l.rpb) * l.ld;
+  const uint32_t rr = (uint32_t)r, rpb = (uint32_t)l.rpb;
+  const uint32_t q = rr / rpb, rem = rr - q * rpb;
+  return (int64_t)q * l.bstride + (int64_t)rem * l.ld;
 }
 
 template <typename T, bool VEC>
@@ -185,6 +188,215 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 fast path (cols % 256 == 0, cols <= 1024, 16-byte aligned rows): a HALF wave (32 lanes)
+// per row, lane l owning the 8-column chunks j*32 + l (j < NJ = cols / 256), so every access is
+// 16 bytes and a wave keeps two rows' loads in flight; reductions are 5 xor-shuffles.
+// ---------------------------------------------------------------------------------------------
+typedef unsigned short us;
+__device__ __forceinline__ float hsum(float v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ void unpack8(const u16x8& u, float* v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = bf2f(u[e]);
+}
+__device__ __forceinline__ u16x8 pack8(const float* v) {
+  u16x8 u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+  return u;
+}
+
+template <int NJ>
+__global__ __launch_bounds__(256) void ln_fwd16_kernel(int rows, int cols, const us* __restrict__ x,
+                                                       mmseq_rows xl, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       us* __restrict__ y, mmseq_rows yl,
+                                                       float* __restrict__ mean,
+                                                       float* __restrict__ rstd, Drop dy_) {
+  const int l = threadIdx.x & 31;
+  const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (r >= rows) return;
+  const us* xr = x + row_off(xl, r);
+  u16x8 raw[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) raw[j] = *reinterpret_cast<const u16x8*>(xr + (j * 32 + l) * 8);
+  float v[NJ][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    unpack8(raw[j], v[j]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[j][e];
+  }
+  const float mu = hsum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[j][e] - mu;
+      q = fmaf(d, d, q);
+    }
+  const float rs = rsqrtf(hsum(q) / cols + eps);
+  us* yr = y + row_off(yl, r);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (j * 32 + l) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c), g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c), b1 = *reinterpret_cast<const f32x4*>(beta + c + 4);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = fmaf((v[j][e] - mu) * rs, g0[e], b0[e]);
+      o[4 + e] = fmaf((v[j][4 + e] - mu) * rs, g1[e], b1[e]);
+    }
+    if (dy_.thr) {
+      float dm[8];
+      drop_mul_pairs<4>(dy_, (uint64_t)r * cols + c, dm);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= dm[e];
+    }
+    *reinterpret_cast<u16x8*>(yr + c) = pack8(o);
+  }
+  if (l == 0) {
+    if (mean) mean[r] = mu;
+    if (rstd) rstd[r] = rs;
+  }
+}
+
+// dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres); RPB16 rows per block,
+// each half wave walks rows hw, hw + 8, ... with the next row's loads issued before the current
+// row's math; per-block dgamma / dbeta partials -> ws[block][2][cols]
+constexpr int RPB16 = 64;
+template <int NJ, bool DIN, bool DXD>
+__global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const us* __restrict__ dy,
+                                                       mmseq_rows dyl, const us* __restrict__ x,
+                                                       mmseq_rows xl, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma,
+                                                       us* __restrict__ dx, mmseq_rows dxl,
+                                                       const us* __restrict__ dres, mmseq_rows dresl,
+                                                       float* __restrict__ ws, Drop din,
+                                                       us* __restrict__ dxd, Drop dout) {
+  __shared__ float red[4][2][NJ * 256];
+  const int l = threadIdx.x & 31, hw = threadIdx.x >> 5;
+  float pg[NJ][8], pb[NJ][8];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pg[j][e] = pb[j][e] = 0.f;
+  const int64_t rbeg = (int64_t)blockIdx.x * RPB16;
+  const int64_t rend = rbeg + RPB16 < rows ? rbeg + RPB16 : rows;
+  auto load_g = [&](int c, float* g8) {
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c), g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { g8[e] = g0[e]; g8[4 + e] = g1[e]; }
+  };
+  // x-hat and g*dy are recomputed in the second pass from the packed row (4 waves per SIMD)
+#pragma unroll 1
+  for (int64_t r = rbeg + hw; r < rend; r += 8) {
+    u16x8 xc[NJ], dc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      xc[j] = *reinterpret_cast<const u16x8*>(x + row_off(xl, r) + (j * 32 + l) * 8);
+      dc[j] = *reinterpret_cast<const u16x8*>(dy + row_off(dyl, r) + (j * 32 + l) * 8);
+    }
+    const float mu = mean[r], rs = rstd[r];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = (j * 32 + l) * 8;
+      float xv[8], d[8], g8[8];
+      unpack8(xc[j], xv);
+      unpack8(dc[j], d);
+      load_g(c, g8);
+      if (DIN) {
+        float dm[8];
+        drop_mul_pairs<4>(din, (uint64_t)r * cols + c, dm);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] *= dm[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xx = (xv[e] - mu) * rs;
+        const float gd = d[e] * g8[e];
+        pg[j][e] = fmaf(d[e], xx, pg[j][e]);
+        pb[j][e] += d[e];
+        s1 += gd;
+        s2 = fmaf(gd, xx, s2);
+      }
+    }
+    s1 = hsum(s1) / cols;
+    s2 = hsum(s2) / cols;
+    us* dxr = dx + row_off(dxl, r);
+    const us* drr = dres ? dres + row_off(dresl, r) : nullptr;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = (j * 32 + l) * 8;
+      float xv[8], d[8], g8[8], o[8];
+      unpack8(xc[j], xv);
+      unpack8(dc[j], d);
+      load_g(c, g8);
+      float dm[8];
+      if (DIN) drop_mul_pairs<4>(din, (uint64_t)r * cols + c, dm);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dd = DIN ? d[e] * dm[e] : d[e];
+        o[e] = rs * (dd * g8[e] - s1 - (xv[e] - mu) * rs * s2);
+      }
+      if (DXD) {
+        float od[8], dm2[8];
+        drop_mul_pairs<4>(dout, (uint64_t)r * cols + c, dm2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) od[e] = o[e] * dm2[e];
+        *reinterpret_cast<u16x8*>(dxd + row_off(dxl, r) + c) = pack8(od);
+      }
+      if (drr) {
+        float t[8];
+        unpack8(*reinterpret_cast<const u16x8*>(drr + c), t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += t[e];
+      }
+      *reinterpret_cast<u16x8*>(dxr + c) = pack8(o);
+    }
+  }
+  // deterministic cross-half-wave reduction in two LDS rounds (keeps LDS at 8 KB per 256 columns)
+  if (hw >= 4) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[hw - 4][0][(j * 32 + l) * 8 + e] = pg[j][e];
+        red[hw - 4][1][(j * 32 + l) * 8 + e] = pb[j][e];
+      }
+  }
+  __syncthreads();
+  if (hw < 4) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[hw][0][(j * 32 + l) * 8 + e] += pg[j][e];
+        red[hw][1][(j * 32 + l) * 8 + e] += pb[j][e];
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const float g = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    const float b = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+    ws[((int64_t)blockIdx.x * 2 + 0) * cols + c] = g;
+    ws[((int64_t)blockIdx.x * 2 + 1) * cols + c] = b;
+  }
+}
+
+bool rows_vec16(const void* p, const mmseq_rows& l) {
+  return ((uintptr_t)p % 16) == 0 && l.ld % 8 == 0 && l.bstride % 8 == 0;
+}
+
 bool rows_vec(const void* p, const mmseq_rows& l, int esz) {
   return ((uintptr_t)p % (4 * esz)) == 0 && l.ld % 4 == 0 && l.bstride % 4 == 0;
 }
@@ -216,6 +428,17 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
   const bool vec = cols % 4 == 0 && rows_vec(x, xl, xd == MMSEQ_BF16 ? 2 : 4) &&
                    rows_vec(y, yl, yd == MMSEQ_BF16 ? 2 : 4);
   const Drop dd = make_drop(drop_y);
+  if (xd == MMSEQ_BF16 && yd == MMSEQ_BF16 && cols % 256 == 0 && rows_vec16(x, xl) &&
+      rows_vec16(y, yl) && ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0) {
+    const dim3 g8((rows + 7) / 8);
+    switch (cols / 256) {
+#define LNF16(NJ) hipLaunchKernelGGL((ln_fwd16_kernel<NJ>), g8, dim3(256), 0, s, rows, cols, \
+                    (const us*)x, xl, gamma, beta, eps, (us*)y, yl, mean, rstd, dd); break
+      case 1: LNF16(1); case 2: LNF16(2); case 3: LNF16(3); case 4: LNF16(4);
+#undef LNF16
+    }
+    return mmseq_check_launch("layernorm_fwd");
+  }
 #define LNF(TX, TY, V)                                                                           \
   hipLaunchKernelGGL((ln_fwd_kernel<TX, TY, V>), grid, dim3(256), 0, s, rows, cols, (const TX*)x, \
                      xl, gamma, beta, eps, (TY*)y, yl, mean, rstd, dd)
@@ -231,7 +454,7 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
 }
 
 extern "C" int64_t mmseq_layernorm_bwd_workspace(int rows, int cols) {
-  const int nb = (rows + RPB - 1) / RPB;
+  const int nb = (rows + RPB16 - 1) / RPB16;  // the bf16 fast path's block count (>= the generic)
   return (int64_t)nb * 2 * cols + mmseq_reduce_extra(nb, 2 * cols);
 }
 
@@ -254,6 +477,30 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
                    rows_vec(dx, dxl, esz) && (!dres || rows_vec(dres, dresl, esz)) &&
                    (!dx_drop || ((uintptr_t)dx_drop % (4 * esz)) == 0);
   const Drop din = make_drop(drop_dy), dout = make_drop(drop_dx);
+  if (dtype == MMSEQ_BF16 && cols % 256 == 0 && rows_vec16(dy, dyl) && rows_vec16(x, xl) &&
+      rows_vec16(dx, dxl) && (!dres || rows_vec16(dres, dresl)) &&
+      (!dx_drop || ((uintptr_t)dx_drop % 16) == 0) && ((uintptr_t)gamma % 16) == 0) {
+    const int nb16 = (rows + RPB16 - 1) / RPB16;
+    const bool di = din.thr != 0, dd = dx_drop != nullptr;
+#define LNB16K(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B>), dim3(nb16), dim3(256), 0, s, rows, \
+                    cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,         \
+                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dout)
+#define LNB16(NJ)                                           \
+  if (di && dd) LNB16K(NJ, true, true);                     \
+  else if (di) LNB16K(NJ, true, false);                     \
+  else if (dd) LNB16K(NJ, false, true);                     \
+  else LNB16K(NJ, false, false);                            \
+  break
+    switch (cols / 256) {
+      case 1: LNB16(1); case 2: LNB16(2); case 3: LNB16(3); case 4: LNB16(4);
+    }
+#undef LNB16
+#undef LNB16K
+    mmseq_status st = mmseq_check_launch("layernorm_bwd");
+    if (st) return st;
+    if (dgamma || dbeta) return ln_reduce_partials(nb16, cols, workspace, dgamma, dbeta, s);
+    return MMSEQ_OK;
+  }
 #define LNB(T, V)                                                                                 \
   hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy,  \
                      dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl, \
