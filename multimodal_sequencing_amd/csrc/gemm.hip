@@ -23,6 +23,7 @@ static float* g_slab = nullptr;
 static int g_ring = 0;  // 1: BK=32 four-slot ring kernel, 0: BK=64 double-buffer kernel
 static int g_big = 1;   // 256 x 256 NT kernel: 1 for large problems, 2 always (tests)
 static int64_t g_slab_bytes = 0;
+static int g_nt_variant = 0;  // large NT: 0 = 256x256 one block/CU, 1 = 256x128 two blocks/CU
 static int g_num_cu = 256;  // persistent grid size (set from the device at first use)
 
 namespace {
@@ -606,7 +607,7 @@ hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s) {
   if (!trans && g_big && a.splitk == 1 && batch == 1 && a.K % 128 == 0 &&
       (g_big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256)) {
     hipError_t e;
-    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, g_num_cu, s, &e)) return e;
+    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, g_num_cu, s, &e, g_nt_variant)) return e;
   }
   const int tiles_m = (a.M + 127) / 128, tiles_n = (a.N + 127) / 128;
   dim3 grid(tiles_m * tiles_n, a.splitk > 1 ? a.splitk : batch);
@@ -632,7 +633,8 @@ extern "C" void mmseq_gemm_set_fast(int enable) {
   // 1 = default (256^2 NT for large problems, double-buffer 128^2 otherwise), 2 = double-buffer
   // 128^2 only, 3 = ring 128^2 only, 4 = 256^2 NT whenever its preconditions hold, 0 = generic
   g_disable_fast = enable == 0;
-  g_big = enable == 1 ? 1 : (enable == 4 ? 2 : 0);
+  g_big = enable == 1 ? 1 : ((enable == 4 || enable == 5) ? 2 : 0);
+  g_nt_variant = enable == 5 ? 1 : 0;
   g_ring = enable == 3;
 }
 

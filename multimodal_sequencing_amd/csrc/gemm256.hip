@@ -23,8 +23,27 @@ __device__ __forceinline__ void st8(us* p, const float* v) {
   *reinterpret_cast<u16x8*>(p) = u;
 }
 
-template <int ACT, bool BWD>
-__device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi) {
+// The epilogue runs in two phases so that no load waits behind a store to a possibly aliasing
+// address (which serialises one full memory round trip per call): epi8_load issues the 16-byte
+// operand reads (dact for BWD, else the residual; plus C when accumulating) of all 16 calls of a
+// wave first, epi8 then computes and stores.
+// one 16-byte operand per call: dact (BWD), else the residual, else C (accumulate); the host
+// never sends the 256 kernels a residual together with accumulate
+struct EpiIn { u16x8 x; };
+template <bool BWD>
+__device__ __forceinline__ EpiIn epi8_load(const GemmArgs& a, int m, int n) {
+  EpiIn in;
+  in.x = (u16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  if (m >= a.M || n >= a.N) return in;
+  const int64_t off = (int64_t)m * a.ldc + n;
+  if (BWD) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.dact) + off);
+  else if (a.resid) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.resid) + (int64_t)m * a.ldr + n);
+  else if (a.accumulate) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.C) + off);
+  return in;
+}
+
+template <int ACT, bool BWD, bool XIN>
+__device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi, const EpiIn& in) {
   if (m >= a.M || n >= a.N) return;
   float v[8];
 #pragma unroll
@@ -42,10 +61,8 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
   }
   const int64_t off = (int64_t)m * a.ldc + n;
   if (BWD) {
-    float d[8];
-    ld8(reinterpret_cast<const us*>(a.dact) + off, d);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] *= act_bwd_fast(ACT, d[r]);
+    for (int r = 0; r < 8; ++r) v[r] *= act_bwd_fast(ACT, bf2f(in.x[r]));
   } else if (ACT) {
     if (a.aux) st8(reinterpret_cast<us*>(a.aux) + off, v);
 #pragma unroll
@@ -57,20 +74,11 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] *= dm[r];
   }
-  if (a.resid) {
-    float t[8];
-    ld8(reinterpret_cast<const us*>(a.resid) + (int64_t)m * a.ldr + n, t);
+  if (XIN && !BWD) {  // residual or C (accumulate); BWD + accumulate is rejected on the host
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] += t[r];
+    for (int r = 0; r < 8; ++r) v[r] += bf2f(in.x[r]);
   }
-  us* cp = reinterpret_cast<us*>(a.C) + off;
-  if (a.accumulate) {
-    float t[8];
-    ld8(cp, t);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] += t[r];
-  }
-  st8(cp, v);
+  st8(reinterpret_cast<us*>(a.C) + off, v);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -108,7 +116,7 @@ __device__ __forceinline__ int g8_of(int X, int q) {
   return 4 + (q & 3) + ((q >> 2) << 3);
 }
 
-template <int ACT, bool BWD>
+template <int ACT, bool BWD, bool XIN>
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF];  // 128 KB
   const int tid = threadIdx.x, lane = tid & 63;
@@ -282,12 +290,38 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
     const int m0 = tm * 256, n0 = tn * 256;
     const int g = lane >> 4, ii = lane & 15;
+    if (ACT < 0) {  // benchmark-only variant: main loop without the epilogue stores
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        epi8<ACT, BWD>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, acc[i][2 * t],
-                       acc[i][2 * t + 1]);
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+      continue;
+    }
+    if (XIN) {  // batches of 4 calls: the operand loads of a batch are issued together
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        EpiIn in[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            in[i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            epi8<ACT, BWD, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[i][t]);
+      }
+    } else {
+      const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          epi8<ACT, BWD, false>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                acc[i][2 * t], acc[i][2 * t + 1], none);
+    }
   }
 #undef FR
 #undef FRB
@@ -448,31 +482,176 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Two-blocks-per-CU NT kernel ("2B"): persistent 256 x 128 tiles, 4 waves (2 x 2, 128 x 64 per
+// wave: the same fragment maps and 16-byte epilogue as above), BK = 32, a 3-stage LDS-DMA ring
+// (24 KB per stage, 72 KB per block), one barrier per 32-deep k-step. Two workgroups share a CU
+// and are NOT barrier-coupled, so one block's epilogue (stores, dropout hashing, residual loads)
+// runs beside the other block's MFMAs instead of stalling the whole CU.
+// Images: A [256][32] and B [128][32] bf16 (64-B rows); 16-B chunk c of row r stored at
+// c ^ (((r >> 3) & 1) << 1): conflict-free for the row-fragment reads of both the plain A rows and
+// the permuted B rows (8 (rho >> 2) + 4 (j & 1) + (rho & 3) + 32 (j >> 1)).
+// ---------------------------------------------------------------------------------------------
+constexpr int S2_STAGE = 256 * 32 + 128 * 32;  // elements per stage
+
+template <int ACT, bool BWD, bool XIN>
+__global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tiles_n, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[3 * S2_STAGE];  // 72 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int G = gridDim.x;
+  const int bid = blockIdx.x;
+  const int first = (G & 7) == 0 ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  const int nk = a.K >> 5;  // 32-deep k-steps per tile
+  const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
+  const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);
+
+  // DMA piece = 16 rows x 64 B: lane -> row (lane >> 2), chunk lane & 3, swizzle ((lane >> 5) & 1) << 1
+  const int sw = ((lane >> 5) & 1) << 1;
+  const uint32_t offA = (uint32_t)((lane >> 2) * a.lda * 2 + (((lane & 3) ^ sw) << 4));
+  const uint32_t offB = (uint32_t)((lane >> 2) * a.ldb * 2 + (((lane & 3) ^ sw) << 4));
+  // stage k-step kk of tile iteration it (kk >= nk: the next tile's k-step kk - nk)
+  auto stage = [&](int it, int kk) {
+    if (kk >= nk) { kk -= nk; ++it; }
+    const int tile = first + it * G;
+    rsrc_t ra, rb;
+    if (tile < ntiles) {
+      const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+      const int m0 = tm * 256, n0 = tn * 128;
+      ra = make_rsrc(Ab + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
+      rb = make_rsrc(Bb + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
+    } else {
+      ra = rb = make_rsrc(Ab, 0);
+    }
+    unsigned short* st = smem + ((it * nk + kk) % 3) * S2_STAGE;  // ring slot of the global step
+    // 24 pieces: 16 of A (rows 16p..), 8 of B; wave w issues pieces w, w + 4, ..., w + 20
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int pc = wave + 4 * e;
+      if (pc < 16)
+        dma16(ra, st + pc * 512, offA + (uint32_t)(((int64_t)pc * 16 * a.lda + kk * 32) * 2));
+      else
+        dma16(rb, st + 256 * 32 + (pc - 16) * 512,
+              offB + (uint32_t)(((int64_t)(pc - 16) * 16 * a.ldb + kk * 32) * 2));
+    }
+  };
+
+  // fragment offsets (elements within a stage): A rows wr*128 + i*16 + l15, chunk g;
+  // B rows wc*64 + 8 (l15 >> 2) + (l15 & 3) + 4 (j & 1) + 32 (j >> 1), chunk g
+  const int l15 = lane & 15, g = lane >> 4;
+  const int hA = ((l15 >> 3) & 1) << 1;
+  const int aoff = (wr * 128 + l15) * 32 + ((g ^ hA) << 3);
+  const int rB = 8 * (l15 >> 2) + (l15 & 3);
+  const int hB = ((rB >> 3) & 1) << 1;  // 4 (j & 1) and 32 (j >> 1) do not change (r >> 3) & 1
+  const int boff = 256 * 32 + (wc * 64 + rB) * 32 + ((g ^ hB) << 3);
+
+  if (first >= ntiles) return;
+  stage(0, 0);
+  stage(0, 1);
+  int it = 0;
+  f32x4 acc[8][4];
+  for (int tile = first; tile < ntiles; tile += G, ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < nk; ++kk) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // k-step kk landed (kk + 1 in flight)
+      __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kk + 2) % 3 no longer read
+      __builtin_amdgcn_sched_barrier(0);
+      stage(it, kk + 2);
+      const unsigned short* st = smem + ((it * nk + kk) % 3) * S2_STAGE;
+      bf16x8_t fa[8], fb[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fa[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(st + aoff + i * 16 * 32));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(
+                                                 st + boff + (4 * (j & 1) + 32 * (j >> 1)) * 32));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m0 = tm * 256, n0 = tn * 128;
+    const int ii = lane & 15;
+    if (XIN) {  // batches of 4 calls: the operand loads of a batch are issued together
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        EpiIn in[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            in[i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            epi8<ACT, BWD, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[i][t]);
+      }
+    } else {
+      const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          epi8<ACT, BWD, false>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                acc[i][2 * t], acc[i][2 * t + 1], none);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
 }  // namespace
 
-bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s, hipError_t* err) {
+bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s, hipError_t* err,
+                      int variant) {
   auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!out_bf16 || a.K % 128 != 0 || a.splitk != 1 || a.N % 8 != 0 || a.ldc % 8 != 0 ||
+      (a.accumulate && (a.resid || a.dact)) ||
       (a.resid && (a.ldr % 8 != 0 || !a16(a.resid))) || !a16(a.C) || (a.aux && !a16(a.aux)) ||
       (a.dact && !a16(a.dact)))
     return false;
-  const int tn = (a.N + 255) / 256;
-  const int ntiles = ((a.M + 255) / 256) * tn;
-  const int grid = ntiles < num_cu ? ntiles : num_cu;
-  const dim3 g(grid), b(512);
+  if (a.act != 0 && a.act != MMSEQ_ACT_GELU_ERF && a.act != MMSEQ_ACT_QUICKGELU) return false;
   const bool bwd = a.dact != nullptr;
-  switch (a.act) {
-    case 0: hipLaunchKernelGGL((gemm256_nt_kernel<0, false>), g, b, 0, s, a, tn, ntiles); break;
-    case MMSEQ_ACT_GELU_ERF:
-      if (bwd) hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, true>), g, b, 0, s, a, tn, ntiles);
-      else hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, false>), g, b, 0, s, a, tn, ntiles);
-      break;
-    case MMSEQ_ACT_QUICKGELU:
-      if (bwd) hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, true>), g, b, 0, s, a, tn, ntiles);
-      else hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, false>), g, b, 0, s, a, tn, ntiles);
-      break;
-    default: return false;
+  const bool xin = bwd || a.resid || a.accumulate;
+  const bool noepi = a.act == 0 && a.alpha == -12345.0f;  // benchmark hook (tools/gemm_epi_bench.py)
+#define NT_DISPATCH(KERNEL, GRID, BLOCK)                                                            \
+  switch (a.act) {                                                                                  \
+    case 0:                                                                                         \
+      if (noepi) hipLaunchKernelGGL((KERNEL<-1, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);  \
+      else if (xin) hipLaunchKernelGGL((KERNEL<0, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles); \
+      else hipLaunchKernelGGL((KERNEL<0, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);         \
+      break;                                                                                        \
+    case MMSEQ_ACT_GELU_ERF:                                                                        \
+      if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles);        \
+      else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles); \
+      else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);         \
+      break;                                                                                        \
+    default:                                                                                        \
+      if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles);        \
+      else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles); \
+      else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);         \
   }
+  if (variant == 1 && a.K % 32 == 0) {  // two 256 x 128 blocks per CU
+    const int tn = (a.N + 127) / 128;
+    const int ntiles = ((a.M + 255) / 256) * tn;
+    const int grid = ntiles < 2 * num_cu ? ntiles : 2 * num_cu;
+    NT_DISPATCH(gemm_nt_2b_kernel, dim3(grid), dim3(256))
+  } else {
+    const int tn = (a.N + 255) / 256;
+    const int ntiles = ((a.M + 255) / 256) * tn;
+    const int grid = ntiles < num_cu ? ntiles : num_cu;
+    NT_DISPATCH(gemm256_nt_kernel, dim3(grid), dim3(512))
+  }
+#undef NT_DISPATCH
   *err = hipGetLastError();
   return true;
 }

@@ -427,7 +427,8 @@ def test_vit_im2col_embed_fwd_bwd(dtype):
                                     (2048, 2304, 128), (164160 // 8, 768, 3072)])
 @pytest.mark.parametrize("epi", ["plain", "gelu_aux", "qgelu_aux", "drop_resid", "dgelu", "dqgelu",
                                  "accum"])
-def test_gemm256_persistent(M, Nn, K, epi):
+@pytest.mark.parametrize("variant", [4, 5])
+def test_gemm256_persistent(M, Nn, K, epi, variant):
     """Persistent 256x256 NT kernel (mode 4 forces it) vs the fp32 reference, and bit-for-bit
     the same dropout mask as the 128x128 path (mode 2) on the same descriptor."""
     g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
@@ -440,7 +441,7 @@ def test_gemm256_persistent(M, Nn, K, epi):
     drop = nat.drop(0.1, 77, 1234) if epi == "drop_resid" else None
     act = {"gelu_aux": 1, "qgelu_aux": 2, "dgelu": 1, "dqgelu": 2}.get(epi, 0)
     outs = []
-    for mode in (4, 2):
+    for mode in (variant, 2):
         nat.gemm_set_fast(mode)
         C = c0.clone()
         aux = torch.empty_like(C) if epi.endswith("aux") else None

@@ -1,0 +1,54 @@
+"""How much of the large NT GEMM time is the epilogue: the path's shapes with/without stores and
+with its fused epilogues (bias+GELU+aux, bias+dropout+residual, dGELU), for both persistent NT
+kernels (mode 4: one 256x256 block per CU, mode 5: two 256x128 blocks per CU)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from multimodal_sequencing_amd import _native as N  # noqa: E402
+
+R = 164160
+
+
+def t(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def main():
+    modes = [int(m) for m in sys.argv[1:]] or [4, 5]
+    for Nn, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        A = torch.randn(R, K, device="cuda").bfloat16()
+        W = (torch.randn(Nn, K, device="cuda") * 0.05).bfloat16()
+        C = torch.empty(R, Nn, device="cuda", dtype=torch.bfloat16)
+        aux = torch.empty_like(C)
+        bias = torch.randn(Nn, device="cuda")
+        res = torch.randn(R, Nn, device="cuda").bfloat16()
+        d = N.drop(0.1, 3, 5)
+        fl = 2.0 * R * Nn * K
+        for mode in modes:
+            N.gemm_set_fast(mode)
+            r = {"mode": mode, "N": Nn, "K": K}
+            if mode == 4:
+                r["noepi"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, alpha=-12345.0)) / 1e12
+            r["plain"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K)) / 1e12
+            r["gelu_aux"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, bias=bias, act=1, aux=aux)) / 1e12
+            r["drop_res"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, bias=bias, resid=res, drop=d)) / 1e12
+            r["dgelu"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, act=1, dact=res)) / 1e12
+            print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}),
+                  flush=True)
+    N.gemm_set_fast(1)
+
+
+if __name__ == "__main__":
+    main()
