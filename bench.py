@@ -73,7 +73,13 @@ class GemmTimer:
                 e0.record(s)
                 orig(A, B, C, M, Nn, K, **kw)
                 e1.record(s)
-                timer.recs.append((e0, e1, 2.0 * M * Nn * K * kw.get("batch", 1)))
+                bt = kw.get("batch", 1)
+                # algorithmic HBM bytes: A, B, C once (+ residual / dact / aux tensors), bf16
+                extra = sum(1 for k in ("resid", "dact", "aux") if kw.get(k) is not None)
+                if kw.get("accumulate"):
+                    extra += 1
+                byts = 2.0 * bt * (M * K + Nn * K + M * Nn * (1 + extra))
+                timer.recs.append((e0, e1, 2.0 * M * Nn * K * bt, byts))
             else:
                 orig(A, B, C, M, Nn, K, **kw)
 
@@ -84,11 +90,27 @@ class GemmTimer:
     def summary(self):
         if not self.recs:
             return None
-        t = sum(e0.elapsed_time(e1) for e0, e1, _ in self.recs) * 1e-3
-        f = sum(fl for _, _, fl in self.recs)
+        t = sum(r[0].elapsed_time(r[1]) for r in self.recs) * 1e-3
+        f = sum(r[2] for r in self.recs)
+        b = sum(r[3] for r in self.recs)
         n = len(self.recs)
         return {"launches": n, "avg_us": t / n * 1e6, "avg_gflop": f / n / 1e9,
-                "achieved_tflops": f / t / 1e12}
+                "achieved_tflops": f / t / 1e12, "avg_alg_bytes": b / n}
+
+
+def pmc_traffic(group="gemm256_nt"):
+    """Per-launch HBM traffic of the roofline kernel from the newest committed rocprofv3 --pmc
+    summary (profiles/r*_pmc_traffic.json, made by tools/pmc_traffic.py: FETCH_SIZE x 2 +
+    WRITE_SIZE, the gfx950 corrections of MI355X_MICROARCH.md), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return d[group]["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def cpu_baseline(preset, seconds_hint=30):
@@ -210,10 +232,14 @@ def main():
     }
     gs = timer.summary()
     if gs:
-        out["roofline"] = {"bound": "mfma", "kernel": "gemm_kernel<bf16,*,NT> (fwd + dgrad)",
+        traffic, tsrc = pmc_traffic()
+        out["roofline"] = {"bound": "mfma", "kernel": "gemm256_nt_kernel (bf16 NT: fwd + dgrad)",
                            "achieved": gs["achieved_tflops"], "peak": PEAK_BF16_TFLOPS,
                            "unit": "TFLOP/s", "frac": gs["achieved_tflops"] / PEAK_BF16_TFLOPS,
-                           "traffic": None, "launches": gs["launches"],
+                           "traffic": traffic, "traffic_unit": "bytes per launch (PMC)",
+                           "traffic_source": tsrc,
+                           "algorithmic_bytes_per_launch": gs["avg_alg_bytes"],
+                           "launches": gs["launches"],
                            "avg_launch_us": gs["avg_us"], "avg_gflop_per_launch": gs["avg_gflop"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

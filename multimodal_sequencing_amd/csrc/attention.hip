@@ -551,6 +551,22 @@ __device__ __forceinline__ rsrc_t head_rsrc(const void* base, int64_t row0, int6
   return make_rsrc(b, ((int64_t)(T - 1) * ld + 64) * 2);
 }
 
+// 1-D grid over (row block, head, pair) with an XCD-aware order: the blocks that share one
+// (pair, head) K/V (or Q/dO) slice get consecutive work indices on ONE XCD (blocks b, b+8, ...
+// share an XCD under round-robin dispatch), so the slice is fetched into that XCD's L2 once.
+struct BlkIdx { int x, h, p; };
+__device__ __forceinline__ BlkIdx attn_block(int nx, int heads) {
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = b & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  BlkIdx r;
+  r.x = w % nx;
+  const int rest = w / nx;
+  r.h = rest % heads;
+  r.p = rest / heads;
+  return r;
+}
+
 // ---- forward ---------------------------------------------------------------------------------
 template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
@@ -559,9 +575,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
-  const int h = blockIdx.y, p = blockIdx.z, T = a.T;
+  const int T = a.T;
+  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const int h = bi.h, p = bi.p;
   const int nkt = (T + 63) >> 6;
-  const int qw = blockIdx.x * 128 + wave * 32;
+  const int qw = bi.x * 128 + wave * 32;
   const bool active = qw < T;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
@@ -706,9 +724,11 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
-  const int h = blockIdx.y, p = blockIdx.z, T = a.T;
+  const int T = a.T;
+  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const int h = bi.h, p = bi.p;
   const int nkt = (T + 63) >> 6;
-  const int qw = blockIdx.x * 128 + wave * 32;
+  const int qw = bi.x * 128 + wave * 32;
   const bool active = qw < T;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
@@ -847,8 +867,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
-  const int h = blockIdx.y, p = blockIdx.z;
-  const int kw = blockIdx.x * 128 + wave * 32;
+  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const int h = bi.h, p = bi.p;
+  const int kw = bi.x * 128 + wave * 32;
   const bool active = kw < T;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
@@ -1029,7 +1050,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MMSEQ_BF16 && g_attn_fast) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
-    const dim3 gq((T + 127) / 128, heads, P);
+    const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4;
     if (a.drop.thr)
       hipLaunchKernelGGL(attn_fwd_bf16_kernel<true>, gq, dim3(256), lds, s, a);
@@ -1069,7 +1090,7 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   if (dtype == MMSEQ_BF16 && g_attn_fast) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0 && aligned16(dqkv) && ld_dqkv % 8 == 0,
                   "attn_bwd: out / dqkv must be 16-byte aligned rows");
-    const dim3 gq((T + 127) / 128, heads, P);
+    const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2;
     if (a.drop.thr) {
       hipLaunchKernelGGL(attn_dq_bf16_kernel<true>, gq, dim3(256), lds, s, a);
