@@ -159,7 +159,12 @@ class BertForOrdering(nn.Module):
         cls_pooled = top[:, 0]  # :1290
         # ---- HierarchicalAttention (:686-817) -------------------------------------------
         t = "two_level_encoder."
-        score = self._lin(self._lin(top, t + "sentence_tran", act=K.TANH), t + "sentence_tran_2")
+        if joint.dtype == torch.bfloat16:  # the head's one large GEMM on the bf16 MFMA kernels
+            st = K.LinearLowpFn.apply(joint[:, :Lt], self._anchor, self.store,
+                                      t + "sentence_tran.weight", t + "sentence_tran.bias", K.TANH)
+        else:
+            st = self._lin(top, t + "sentence_tran", act=K.TANH)
+        score = self._lin(st, t + "sentence_tran_2")
         mix = K.SpanPoolFn.apply(top, score.view(P, Lt), sep_positions.reshape(P, 2).contiguous(),
                                  D.site(ph, "span"))  # :735
         sample = mix.view(B, 2 * npair, H)[:, mp["slot"]].view(B, N, mp["E"], H)

@@ -397,6 +397,51 @@ class LinearFn(torch.autograd.Function):
         return dx, None, None, None, None, None
 
 
+class LinearLowpFn(torch.autograd.Function):
+    """y (fp32) = act(x W^T + b) for an fp32-stored head weight applied to a compute-dtype (bf16)
+    activation: the GEMMs run on the bf16 MFMA kernels with a per-call bf16 copy of W (and of
+    W^T for the dgrad), the fp32 gradient is accumulated into the store. Used in bf16 mode for
+    the one large head projection (HierarchicalAttention.sentence_tran over every text token,
+    modeling_bert.py:697-699); parity (fp32) mode keeps LinearFn."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, store, wname, bname, act):
+        x = x.contiguous()
+        shp = x.shape
+        x2 = x.view(-1, shp[-1])
+        W32 = store.f32(wname)
+        Wb = torch.empty(W32.shape, device=x.device, dtype=x.dtype)
+        N.cast(W32, Wb)
+        aux = torch.empty(x2.shape[0], W32.shape[0], device=x.device) if act else None
+        y = _linear(x2, Wb, bias=store.f32(bname) if bname else None, act=act, aux=aux,
+                    out_dtype=torch.float32)
+        ctx.save_for_backward(x2, aux if act else None)
+        ctx.meta = (store, wname, bname, act, shp)
+        return y.view(*shp[:-1], W32.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, aux = ctx.saved_tensors
+        store, wname, bname, act, shp = ctx.meta
+        dy = dy.contiguous().view(-1, dy.shape[-1])
+        if act:
+            dz = torch.empty_like(dy)
+            N.act_bwd(aux, dy, dz, act)
+            dy = dz
+        if bname:
+            _colsum(dy, store.g(bname))
+        dyb = torch.empty(dy.shape, device=dy.device, dtype=x2.dtype)
+        N.cast(dy, dyb)
+        _wgrad(dyb, x2, store.g(wname))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            W32 = store.f32(wname)
+            WTb = torch.empty(W32.shape[1], W32.shape[0], device=dy.device, dtype=x2.dtype)
+            N.transpose_cast(W32, WTb)
+            dx = _dgrad(dyb, WTb).view(shp)
+        return dx, None, None, None, None, None
+
+
 class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, store, prefix, eps):
