@@ -84,6 +84,13 @@ void mmseq_gemm_set_fast(int enable);
  * the slabs in a fixed order (bitwise reproducible). The workspace must not be used concurrently
  * by GEMMs on different streams. NULL disables split-K. */
 void mmseq_gemm_set_workspace(void* ws, int64_t bytes);
+/* Weight + bias gradient of a Linear in one pass (replaces the wgrad GEMM and the bias column sum
+ * of every nn.Linear backward on the path): C[M][N] += sum_k A[k][m] B[k][n] (A = dY [K][lda],
+ * B = X [K][ldb], fp32 C) and, if bias_grad != NULL, bias_grad[m] += sum_k A[k][m] (fp32).
+ * Deterministic (fixed-order split-K reductions). */
+mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int64_t lda, const void* B,
+                              int64_t ldb, float* C, int64_t ldc, float* bias_grad,
+                              mmseq_dtype in_dtype, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused multi-head attention over a packed QKV activation (lxrt/modeling.py:398-425 with the

@@ -62,6 +62,8 @@ _SIGS = {
                                                        _dp, _vp]),
     "mmseq_gemm_set_fast": (None, [ctypes.c_int]),
     "mmseq_attn_set_fast": (None, [ctypes.c_int]),
+    "mmseq_gemm_wgrad": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _c_i64, _vp, _c_i64,
+                                                             _vp, ctypes.c_int, _vp]),
     "mmseq_gemm_set_workspace": (None, [_vp, _c_i64]),
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
@@ -189,6 +191,17 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
     _check(lib().mmseq_gemm(trans, M, N, K, batch, _p(A), lda, sA, _p(B), ldb, sB, _p(C), ldc, sC,
                             _p(bias), act, _p(aux), _p(dact), _p(resid), ldr, sR, alpha,
                             int(accumulate), dt(A), dt(C), _d(drop), _stream()), "mmseq_gemm")
+
+
+def gemm_wgrad(dy, x, gW, gb=None):
+    """gW[out][in] += dy^T x and gb[out] += column sums of dy (fp32), dy [R][out], x [R][in]."""
+    _dev(dy, x, gW)
+    if not _ws:
+        ensure_gemm_workspace(dy.device)
+    M, Nn = gW.shape
+    R = dy.numel() // dy.shape[-1]
+    _check(lib().mmseq_gemm_wgrad(M, Nn, R, _p(dy), dy.shape[-1], _p(x), x.shape[-1], _p(gW), Nn,
+                                  _p(gb), dt(dy), _stream()), "mmseq_gemm_wgrad")
 
 
 def gemm_set_fast(enable):

@@ -572,6 +572,27 @@ __global__ __launch_bounds__(256, 2) void gemm_ring_kernel(GemmArgs a, int tiles
 }
 
 // C[m][n] (+)= sum_s slab[s][m][n], fixed order (bitwise reproducible)
+// out[m] += sum_s slab[s][m] (fused bias-gradient partials of the split-K wgrad; fixed order)
+__global__ __launch_bounds__(256) void cs_reduce_kernel(int M, int S, const float* __restrict__ slab,
+                                                        float* __restrict__ out) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += slab[(int64_t)s * M + m];
+  out[m] += v;
+}
+
+// out[m] += sum_k A[k][m] (fallback bias gradient when the fused path is not eligible)
+template <typename TI>
+__global__ __launch_bounds__(256) void colsum_simple_kernel(int M, int K, const TI* __restrict__ A,
+                                                            int64_t lda, float* __restrict__ out) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float v = 0.f;
+  for (int k = 0; k < K; ++k) v += Elem<TI>::ld(A + (int64_t)k * lda + m);
+  out[m] += v;
+}
+
 // C[m][n] (+)= sum_s slab[s][m][n] for any N (element-wise; the generic split-K path)
 __global__ __launch_bounds__(256) void splitk_reduce1_kernel(int M, int N, int S, const float* __restrict__ slab,
                                                              float* __restrict__ C, int64_t ldc,
@@ -692,6 +713,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
                        (trans ? (M % 8 == 0 && N % 8 == 0) : (K % 64 == 0)) &&
                        (int64_t)M * N >= 128 * 128;
   a.splitk = 1; a.kchunk = K; a.slab = nullptr;
+  a.cs = nullptr; a.cs_slab = nullptr;
   if (fast_ok) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     const bool plain = !bias && !act && !aux_out && !dact_aux && !resid && alpha == 1.0f &&
@@ -788,4 +810,62 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
     e = launch<float, unsigned short>(trans, a, batch, s);
   if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm launch: %s", hipGetErrorString(e));
   return MMSEQ_OK;
+}
+
+// Weight gradient with the fused bias gradient (include/mmseq.h): C[M][N] += A^T B and
+// bias_grad[m] += sum_k A[k][m]. bf16 operands with an eligible shape take the 256 x 256 TN
+// kernel (column sums of the A fragments on the VALU beside the MFMAs); anything else runs
+// mmseq_gemm plus a separate column-sum kernel.
+extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int64_t lda,
+                                         const void* B, int64_t ldb, float* C, int64_t ldc,
+                                         float* bias_grad, mmseq_dtype in_dtype,
+                                         mmseq_stream stream) {
+  MMSEQ_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_wgrad: bad sizes");
+  MMSEQ_REQUIRE(A && B && C, "gemm_wgrad: null operand");
+  MMSEQ_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gemm_wgrad: ld too small");
+  MMSEQ_REQUIRE(in_dtype == MMSEQ_F32 || in_dtype == MMSEQ_BF16, "gemm_wgrad: bad dtype");
+  if (M == 0 || N == 0 || K == 0) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (in_dtype == MMSEQ_BF16 && g_big && bias_grad) {
+    GemmArgs t = {};
+    t.M = M; t.N = N; t.K = K;
+    t.A = A; t.lda = lda; t.B = B; t.ldb = ldb; t.C = C; t.ldc = ldc;
+    t.alpha = 1.f; t.accumulate = 1;
+    t.drop = make_drop(nullptr);
+    const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+    int S2 = t256 < g_num_cu ? g_num_cu / t256 : 1;
+    if (S2 > K / 1024) S2 = K / 1024 > 0 ? K / 1024 : 1;
+    while (S2 > 1 && (!g_slab || (int64_t)S2 * (M + (int64_t)M * N) * 4 > g_slab_bytes)) --S2;
+    t.splitk = S2;
+    t.kchunk = ((K + S2 - 1) / S2 + 127) / 128 * 128;
+    t.splitk = (K + t.kchunk - 1) / t.kchunk;
+    if (t.splitk <= 1) { t.splitk = 1; t.kchunk = K; }
+    t.slab = g_slab;
+    t.cs = bias_grad;
+    t.cs_slab = t.splitk > 1 ? g_slab + (int64_t)t.splitk * M * N : nullptr;
+    hipError_t e2 = hipSuccess;
+    if (mmseq_gemm256_tn(t, s, &e2)) {
+      if (e2 == hipSuccess && t.splitk > 1) {
+        const int64_t t4 = (int64_t)M * N / 4;
+        const unsigned blocks = (unsigned)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, M, N, t.splitk,
+                           g_slab, C, ldc, 1);
+        hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, t.splitk,
+                           t.cs_slab, bias_grad);
+        e2 = hipGetLastError();
+      }
+      if (e2 != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_wgrad: %s", hipGetErrorString(e2));
+      return MMSEQ_OK;
+    }
+  }
+  mmseq_status st = mmseq_gemm(1, M, N, K, 1, A, lda, 0, B, ldb, 0, C, ldc, 0, nullptr, 0, nullptr,
+                               nullptr, nullptr, 0, 0, 1.0f, 1, in_dtype, MMSEQ_F32, nullptr, stream);
+  if (st || !bias_grad) return st;
+  if (in_dtype == MMSEQ_BF16)
+    hipLaunchKernelGGL(colsum_simple_kernel<unsigned short>, dim3((M + 255) / 256), dim3(256), 0, s,
+                       M, K, (const unsigned short*)A, lda, bias_grad);
+  else
+    hipLaunchKernelGGL(colsum_simple_kernel<float>, dim3((M + 255) / 256), dim3(256), 0, s, M, K,
+                       (const float*)A, lda, bias_grad);
+  return mmseq_check_launch("gemm_wgrad colsum");
 }

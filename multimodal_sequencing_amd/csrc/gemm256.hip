@@ -415,6 +415,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   bf16x8_t fa[8], fb[4];
+  // fused bias gradient (column sums of A = dY): blocks of the first column tile only; wave wc
+  // sums A tiles i = wc (cs0) and 4 + wc (cs1) on the VALU beside its MFMAs; lane (g, ii) holds
+  // the partial over its k-slots of column wr*128 + i*16 + ii
+  const bool do_cs = a.cs != nullptr && tn == 0;
+  float cs0 = 0.f, cs1 = 0.f;
+  bf16x8_t fcs;  // the wave's bias-gradient fragment: one extra transposed read per phase
+  const int fAc0 = kr * 256 + (((wr * 16 + 2 * wc + (pp >> 1)) ^ (t8 << 1)) << 3) + (pp & 1) * 4;
+  const int fAc1 = kr * 256 + (((wr * 16 + 2 * (4 + wc) + (pp >> 1)) ^ (t8 << 1)) << 3) + (pp & 1) * 4;
+  auto cs_add = [&](float& dst) {
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    const u32x4 u = __builtin_bit_cast(u32x4, fcs);
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t += __uint_as_float(u[e] << 16) + __uint_as_float(u[e] & 0xFFFF0000u);
+    dst += t;
+  };
 
   stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
   stage(1, 1); stage(1, 0);
@@ -424,6 +440,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
 
 #define TN_PHASE(READS, STAGE, VMWAIT, I0, KS)                                          \
   READS;                                                                                \
+  if (do_cs) fcs = frag(buf + (KS) * 32 * 256 + ((I0) ? fAc1 : fAc0));                  \
   STAGE;                                                                                \
   __builtin_amdgcn_sched_barrier(0);                                                    \
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                          \
@@ -435,6 +452,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
   _Pragma("unroll") for (int j = 0; j < 4; ++j)                                         \
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);                                                        \
+  if (do_cs) cs_add((I0) ? cs1 : cs0);                                                  \
   __builtin_amdgcn_sched_barrier(0);                                                    \
   __builtin_amdgcn_s_barrier();
 
@@ -464,6 +482,23 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
   if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  if (do_cs) {
+    cs0 += __shfl_xor(cs0, 16, 64);
+    cs0 += __shfl_xor(cs0, 32, 64);
+    cs1 += __shfl_xor(cs1, 16, 64);
+    cs1 += __shfl_xor(cs1, 32, 64);
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int m = m0 + wr * 128 + (q * 4 + wc) * 16 + ii;
+        const float v = q ? cs1 : cs0;
+        if (m < a.M) {
+          if (a.splitk > 1) a.cs_slab[(int64_t)split * a.M + m] = v;
+          else a.cs[m] += v;
+        }
+      }
+    }
+  }
   float* C = a.splitk > 1 ? a.slab + (int64_t)split * a.M * a.N : reinterpret_cast<float*>(a.C);
   const int64_t ldc = a.splitk > 1 ? a.N : a.ldc;
   const bool acc_c = a.splitk == 1 && a.accumulate;

@@ -14,6 +14,8 @@ struct GemmArgs {
   float alpha; int accumulate; int vec_ok; int vec_c;
   int splitk; int kchunk; float* slab;  // split-K (TN wgrad): partial slabs [splitk][M][N] f32
   Drop drop;                            // dropout after the activation, before the residual
+  float* cs;       // TN wgrad: fused bias gradient cs[m] += sum_k A[k][m] (nullptr: off)
+  float* cs_slab;  // ... per-split partials [splitk][M] when splitk > 1
 };
 
 template <typename TO>

@@ -27,8 +27,12 @@ def _colsum(x, out):
     N.colsum(x, rows, x.shape[-1], x.shape[-1], out, accumulate=True)
 
 
-def _wgrad(dy, x, gW):
-    """gW[out][in] += dy^T x  (dy [R][out], x [R][in]) — TN GEMM accumulating in fp32."""
+def _wgrad(dy, x, gW, gb=None):
+    """gW[out][in] += dy^T x  (dy [R][out], x [R][in]) — TN GEMM accumulating in fp32; with gb the
+    bias gradient gb[out] += sum_r dy[r] is fused into the same pass (mmseq_gemm_wgrad)."""
+    if gb is not None:
+        N.gemm_wgrad(dy, x, gW, gb)
+        return
     R = dy.numel() // dy.shape[-1]
     N.gemm(dy, x, gW, gW.shape[0], gW.shape[1], R, trans=1, lda=dy.shape[-1], ldb=x.shape[-1],
            accumulate=True)
@@ -138,12 +142,10 @@ class BertLayerFn(torch.autograd.Function):
         N.layernorm_bwd(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
                         None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b),
                         dx_drop=ds2d if d_out is not None else None, drop_dx=d_out)
-        _wgrad(ds2d, gact, st.g(L.out_w))
-        _colsum(ds2d, st.g(L.out_b))
+        _wgrad(ds2d, gact, st.g(L.out_w), st.g(L.out_b))
         dz = _dgrad(ds2d, st.wt(L.out_w), act=GELU, dact=z)
         del ds2d
-        _wgrad(dz, h1, st.g(L.i_w))
-        _colsum(dz, st.g(L.i_b))
+        _wgrad(dz, h1, st.g(L.i_w), st.g(L.i_b))
         dh1 = _dgrad(dz, st.wt(L.i_w), resid=ds2)
         del dz
         ds1 = torch.empty_like(dy)
@@ -151,16 +153,14 @@ class BertLayerFn(torch.autograd.Function):
         N.layernorm_bwd(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
                         None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
                         dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
-        _wgrad(ds1d, o, st.g(L.o_w))
-        _colsum(ds1d, st.g(L.o_b))
+        _wgrad(ds1d, o, st.g(L.o_w), st.g(L.o_b))
         do = _dgrad(ds1d, st.wt(L.o_w))
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
         N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
                    H, do, H, lse, delta, dqkv, 3 * H, drop=d_att)
-        _wgrad(dqkv, x, st.packed(L.qkv_w, "g"))
-        _colsum(dqkv, st.packed(L.qkv_b, "g").view(-1))
+        _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None
 
@@ -205,25 +205,21 @@ class VitBlockFn(torch.autograd.Function):
         W = h.shape[-1]
         R = h.shape[0]
         dx2 = dx2.contiguous()
-        _wgrad(dx2, gact, st.g(L.proj_w))
-        _colsum(dx2, st.g(L.proj_b))
+        _wgrad(dx2, gact, st.g(L.proj_w), st.g(L.proj_b))
         dz = _dgrad(dx2, st.wt(L.proj_w), act=QGELU, dact=z)
-        _wgrad(dz, hn2, st.g(L.fc_w))
-        _colsum(dz, st.g(L.fc_b))
+        _wgrad(dz, hn2, st.g(L.fc_w), st.g(L.fc_b))
         dhn2 = _dgrad(dz, st.wt(L.fc_w))
         del dz
         dx1 = torch.empty_like(h)
         N.layernorm_bwd(R, W, dhn2, _rows(W), x1, _rows(W), m2, r2, st.f32(L.ln2_w), dx1, _rows(W),
                         dx2, _rows(W), st.g(L.ln2_w), st.g(L.ln2_b))
-        _wgrad(dx1, o, st.g(L.out_w))
-        _colsum(dx1, st.g(L.out_b))
+        _wgrad(dx1, o, st.g(L.out_w), st.g(L.out_b))
         do = _dgrad(dx1, st.wt(L.out_w))
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=h.device)
         N.attn_bwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
                    do, W, lse, delta, dqkv, 3 * W)
-        _wgrad(dqkv, hn, st.g(L.in_w))
-        _colsum(dqkv, st.g(L.in_b))
+        _wgrad(dqkv, hn, st.g(L.in_w), st.g(L.in_b))
         dhn = _dgrad(dqkv, st.wt(L.in_w))
         dh = torch.empty_like(h)
         N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
@@ -353,8 +349,7 @@ class JointInputFn(torch.autograd.Function):
             N.layernorm_bwd(P * Tv, H, djoint[Lt:], N.rows(H, T * H, Tv), vpre, _rows(H), mv, rv,
                             st.f32(L.vln_w), dvpre, _rows(H), None, _rows(H), st.g(L.vln_w),
                             st.g(L.vln_b), drop_dy=drops[1])
-            _wgrad(dvpre, vout, st.g(L.v_w))
-            _colsum(dvpre, st.g(L.v_b))
+            _wgrad(dvpre, vout, st.g(L.v_w), st.g(L.v_b))
             dvout = _dgrad(dvpre, st.wt(L.v_w))
         return dvout, None, None, None, None, None, None, None, None, None, None, None
 

@@ -501,3 +501,30 @@ def test_gemm_fp32_splitk(trans, M, N, K):
     ref = C0.double() + (A.double().t() @ B.double() if trans else A.double() @ B.double().t())
     err = (C.double() - ref).abs().max().item()
     assert err <= 1e-5 * math.sqrt(K) * (1 + ref.abs().max().item()) / 8, err
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 3072, 20000), (2304, 768, 4100), (768, 768, 164), (40, 96, 300),
+                                   (3072, 768, 1000)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_wgrad_fused_bias(M, N, K, dtype):
+    """mmseq_gemm_wgrad: dW += dY^T X and db += colsum(dY) in one pass (split-K, fused column sums
+    on the bf16 256x256 TN kernel; fallback path otherwise); deterministic."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    dY = torch.randn(K, M, generator=g).to(DEV, dtype)
+    X = torch.randn(K, N, generator=g).to(DEV, dtype)
+    W0 = torch.randn(M, N, generator=g).to(DEV)
+    b0 = torch.randn(M, generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        gW, gb = W0.clone(), b0.clone()
+        nat.gemm_wgrad(dY, X, gW, gb)
+        outs.append((gW, gb))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    refW = W0.double() + dY.double().t() @ X.double()
+    refb = b0.double() + dY.double().sum(0)
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    errW = (outs[0][0].double() - refW).abs().max().item()
+    errb = (outs[0][1].double() - refb).abs().max().item()
+    assert errW <= tol * math.sqrt(K) * (1 + refW.abs().max().item()), errW
+    assert errb <= tol * math.sqrt(K) * (1 + refb.abs().max().item()), errb
