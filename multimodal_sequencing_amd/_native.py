@@ -68,10 +68,11 @@ _SIGS = {
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            ctypes.c_int, _dp, _vp]),
+    "mmseq_attn_keep_bits_words": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            _c_i64, _vp, _vp, _vp, _c_i64,
-                                                           ctypes.c_int, _dp, _vp]),
+                                                           ctypes.c_int, _dp, _vp, _vp]),
     "mmseq_small_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 4 + [ctypes.c_float, _vp,
                                                                              _vp, _dp, _vp]),
     "mmseq_small_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float, _vp,
@@ -222,11 +223,17 @@ def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out
            "mmseq_attn_fwd")
 
 
+def attn_keep_bits(P, T, heads, device):
+    """Backward workspace for the attention-dropout keep mask as bits (dQ writes, dK/dV reads)."""
+    return torch.empty(lib().mmseq_attn_keep_bits_words(P, T, heads), dtype=torch.int64,
+                       device=device)
+
+
 def attn_bwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, dout,
-             ld_dout, lse, delta, dqkv, ld_dqkv, drop=None):
+             ld_dout, lse, delta, dqkv, ld_dqkv, drop=None, keep_bits=None):
     _check(lib().mmseq_attn_bwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
                                 scale, _p(out), ld_out, _p(dout), ld_dout, _p(lse), _p(delta),
-                                _p(dqkv), ld_dqkv, dt(qkv), _d(drop), _stream()),
+                                _p(dqkv), ld_dqkv, dt(qkv), _d(drop), _p(keep_bits), _stream()),
            "mmseq_attn_bwd")
 
 

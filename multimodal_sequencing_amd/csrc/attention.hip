@@ -41,6 +41,8 @@ struct AttnArgs {
   void* dqkv; int64_t ld_dqkv;
   void* o_w;  // fwd output
   Drop drop;  // attention-probability dropout
+  uint64_t* bits;  // bf16 fast path: keep-mask words [(p*heads+h)*T + q][nkt2], bit j = key 64*kt + j
+  int nkt2;        // key tiles per row, rounded up to even (16-byte rows for the dK/dV staging)
 };
 
 // Stage rows [r0, r0+64) of one head's 64-wide slice into LDS tile s ([64][LD]); zero-fill >= T.
@@ -568,8 +570,9 @@ __device__ __forceinline__ BlkIdx attn_block(int nx, int heads) {
 }
 
 // ---- forward ---------------------------------------------------------------------------------
-template <bool DROP>
+template <int DMODE>  // dropout: 0 none, 1 counter hash
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
+  constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
   float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -717,8 +720,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
 }
 
 // ---- backward: dQ (per 128-query block, keys swept), also writes delta = rowsum(dO * O) --------
-template <bool DROP>
+template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep-bit words for dK/dV
 __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
+  constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
   float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -817,12 +821,17 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     for (int kb = 0; kb < 4; ++kb)
       bias[kb] = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 16 + 4 * g);
     bf16x8_t dsf[2][2];
+    uint32_t kb16[2] = {0u, 0u};  // keep bits: 16-bit slice g of the tile word, bit kb*4 + r
 #pragma unroll
     for (int grp = 0; grp < 2; ++grp) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         float dm[4] = {1.f, 1.f, 1.f, 1.f};
         if (DROP) drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
+        if (DMODE == 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kb16[grp] |= (dm[r] != 0.f ? 1u : 0u) << (kb * 4 + r);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float pv = ex2(fmaf(s[grp][kb][r], c, bias[kb][r]) - L2[grp]);
@@ -831,6 +840,12 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
       }
       dsf[grp][0] = pack_pair(dp[grp][0], dp[grp][1]);
       dsf[grp][1] = pack_pair(dp[grp][2], dp[grp][3]);
+      if (DMODE == 2) {
+        const int q = qw + grp * 16 + i;
+        if (q < T)
+          reinterpret_cast<unsigned short*>(a.bits)[((((int64_t)p * a.heads + h) * T + q) * a.nkt2 + t) * 4 + g] =
+              (unsigned short)kb16[grp];
+      }
     }
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -857,13 +872,16 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
 }
 
 // ---- backward: dK, dV (per 128-key block, queries swept; key on the MFMA lane) ----------------
-template <bool DROP>
+template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep-bit words from the dQ kernel
 __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
+  constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (Q, dO) + lse, D
   const int T = a.T;
   const int nqt = (T + 63) >> 6;
   float* sL = reinterpret_cast<float*>(smem + 4 * IMG);
   float* sD = sL + nqt * 64;
+  // keep-bit words of the q-tile for this block's two key tiles: [2 buffers][64 q][4 dwords]
+  unsigned short* sBits = reinterpret_cast<unsigned short*>(sD + nqt * 64);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
@@ -875,6 +893,10 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
   const rsrc_t ro = head_rsrc(a.dout, (int64_t)p * T, a.ld_dout, h * 64, T);
   const uint32_t loffq = dma_lane_off(lane, ld), loffo = dma_lane_off(lane, a.ld_dout);
+  const int64_t bh = (int64_t)p * a.heads + h;
+  const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + bh * T * a.nkt2, (int64_t)T * a.nkt2 * 8)
+                                  : make_rsrc(a.qkv, 0);
+  const int kt0 = 2 * bi.x;  // this block's first key tile
   auto stage = [&](int t) {
     unsigned short* qimg = smem + (t & 1) * 2 * IMG;
 #pragma unroll
@@ -883,6 +905,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
       dma16(rq, qimg + pc * 512, loffq + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2));
       dma16(ro, qimg + IMG + pc * 512, loffo + (uint32_t)((int64_t)(t * 64 + pc * 8) * a.ld_dout * 2));
     }
+    if (DMODE == 2 && wave == 0)  // 64 rows x 16 B: words (kt0, kt0 + 1) of queries t*64 + lane
+      dma16(rbits, sBits + (t & 1) * 512,
+            (uint32_t)((((int64_t)(t * 64 + lane)) * a.nkt2 + kt0) * 8));
   };
   stage(0);
   const int64_t rb = ((int64_t)p * a.heads + h) * T;
@@ -929,7 +954,28 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     // dropout keep-bits of this lane's 32 (q, key) elements, bit grp*16 + qs*4 + r, computed
     // before the MFMAs (few live registers); (q, key) -> index (rb + q) * Tp2 + key
     uint32_t keep = 0xFFFFFFFFu;
-    if (DROP) {
+    if (DMODE == 2) {
+      // word (kt0 + (wave >> 1)) of a row holds this wave's keys; key j (0..63 in its tile) sits
+      // at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3) (16-bit slice per forward lane group)
+      keep = 0;
+      const uint64_t* bw = reinterpret_cast<const uint64_t*>(sBits + (t & 1) * 512) + (wave >> 1);
+      int pos[2];
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        const int j = (wave & 1) * 32 + grp * 16 + i;
+        pos[grp] = ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3);
+      }
+#pragma unroll
+      for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint64_t w = bw[(qs * 16 + 4 * g + r) * 2];
+#pragma unroll
+          for (int grp = 0; grp < 2; ++grp)
+            keep |= (uint32_t)((w >> pos[grp]) & 1u) << (grp * 16 + qs * 4 + r);
+        }
+    }
+    if (DMODE == 1) {
       keep = 0;
       const uint64_t dbase = (uint64_t)(rb + t * 64 + 4 * g) * (uint64_t)Tp2 + kw + i;
 #pragma unroll
@@ -1053,9 +1099,9 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4;
     if (a.drop.thr)
-      hipLaunchKernelGGL(attn_fwd_bf16_kernel<true>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel<1>, gq, dim3(256), lds, s, a);
     else
-      hipLaunchKernelGGL(attn_fwd_bf16_kernel<false>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel<0>, gq, dim3(256), lds, s, a);
   } else if (dtype == MMSEQ_BF16)
     hipLaunchKernelGGL(attn_fwd_kernel<unsigned short>, grid, dim3(256), 0, s, a);
   else
@@ -1069,7 +1115,8 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
                                        int64_t ld_out, const void* dout, int64_t ld_dout,
                                        const float* lse, float* delta, void* dqkv,
                                        int64_t ld_dqkv, mmseq_dtype dtype,
-                                       const mmseq_dropout* drop, mmseq_stream stream) {
+                                       const mmseq_dropout* drop, uint64_t* keep_bits,
+                                       mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   const int ve = dtype == MMSEQ_BF16 ? 8 : 4;
@@ -1091,13 +1138,18 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0 && aligned16(dqkv) && ld_dqkv % 8 == 0,
                   "attn_bwd: out / dqkv must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
-    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2;
-    if (a.drop.thr) {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<true>, gq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<true>, gq, dim3(256), lds, s, a);
+    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2 + 2048;
+    a.bits = keep_bits;
+    a.nkt2 = (((T + 63) / 64) + 1) & ~1;
+    if (a.drop.thr && keep_bits) {
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<2>, gq, dim3(256), lds, s, a);
+    } else if (a.drop.thr) {
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<1>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<1>, gq, dim3(256), lds, s, a);
     } else {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<false>, gq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<false>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<0>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<0>, gq, dim3(256), lds, s, a);
     }
   } else if (dtype == MMSEQ_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<unsigned short>, gd, dim3(256), 0, s, a);
@@ -1112,3 +1164,8 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
 }
 
 extern "C" void mmseq_attn_set_fast(int enable) { g_attn_fast = enable != 0; }
+
+extern "C" int64_t mmseq_attn_keep_bits_words(int P, int T, int heads) {
+  const int64_t nkt2 = (((T + 63) / 64) + 1) & ~1;
+  return (int64_t)P * heads * T * nkt2;
+}

@@ -158,8 +158,11 @@ class BertLayerFn(torch.autograd.Function):
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
+        # dropout keep mask as bits: written by the dQ kernel, read by the dK/dV kernel
+        kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None else None
         N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
-                   H, do, H, lse, delta, dqkv, 3 * H, drop=d_att)
+                   H, do, H, lse, delta, dqkv, 3 * H, drop=d_att, keep_bits=kbits)
+        del kbits
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None

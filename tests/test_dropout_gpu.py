@@ -103,8 +103,9 @@ def test_layernorm_dropout_fwd_bwd(dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("P,T,heads,masked", [(2, 129, 2, True), (1, 513, 3, True),
-                                              (2, 64, 1, False)])
-def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked):
+                                              (2, 64, 1, False), (1, 200, 2, False)])
+@pytest.mark.parametrize("bits", [False, True])
+def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked, bits):
     g = torch.Generator(device="cpu").manual_seed(T + heads)
     H = heads * 64
     qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, dtype)
@@ -117,6 +118,7 @@ def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked):
     scale = 1 / 8
     out = torch.empty(P * T, H, device=DEV, dtype=dtype)
     lse = torch.empty(P, heads, T, device=DEV)
+    kb = nat.attn_keep_bits(P, T, heads, DEV) if bits else None
     nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse, drop=d)
     Tp2 = (T + 1) & ~1  # attention mask rows are laid out with an even stride
     Mk = _mask((P, heads, T, Tp2), d)[..., :T]
@@ -133,7 +135,14 @@ def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked):
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(P, heads, T, device=DEV)
     nat.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, dout, H, lse, delta,
-                 dqkv, 3 * H, drop=d)
+                 dqkv, 3 * H, drop=d, keep_bits=kb)
+    if bits and dtype == torch.bfloat16:  # the stored keep bits are exactly the counter mask
+        nkt2 = kb.numel() // (P * heads * T)
+        w = kb.view(P, heads, T, nkt2, 1)
+        j = torch.arange(64, device=DEV)
+        sh = (((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3)).view(1, 1, 1, 1, 64)
+        keep = ((w >> sh) & 1).view(P, heads, T, nkt2 * 64)[..., :T]
+        assert torch.equal(keep.bool(), Mk != 0)
     (rg,) = torch.autograd.grad(ref, qf, dout.float())
     torch.testing.assert_close(dqkv.float(), rg, rtol=2 * tol, atol=2 * tol)
 

@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodal_sequencing_amd import _native as N
 
 
-def run(P, T, heads, drop, iters=5):
+def run(P, T, heads, drop, iters=5, bits=False):
     H = heads * 64
     g = torch.Generator(device="cpu").manual_seed(0)
     qkv = (torch.randn(P * T, 3 * H, generator=g) * 0.5).to("cuda", torch.bfloat16)
@@ -16,9 +16,10 @@ def run(P, T, heads, drop, iters=5):
     delta = torch.empty_like(lse)
     dqkv = torch.empty_like(qkv)
     d = N.drop(0.1, 5, 99) if drop else None
+    kb = N.attn_keep_bits(P, T, heads, "cuda") if bits else None
     fwd = lambda: N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, lse, drop=d)
     bwd = lambda: N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, dout, H,
-                             lse, delta, dqkv, 3 * H, drop=d)
+                             lse, delta, dqkv, 3 * H, drop=d, keep_bits=kb)
     res = {}
     for name, f in (("fwd", fwd), ("bwd", bwd)):
         f(); torch.cuda.synchronize()
@@ -34,5 +35,6 @@ def run(P, T, heads, drop, iters=5):
 
 
 for P, T in ((320, 513), (320, 393)):
-    for drop in (False, True):
-        print(json.dumps({"P": P, "T": T, "drop": drop, **run(P, T, 12, drop)}), flush=True)
+    for drop, bits in ((False, False), (True, False), (True, True)):
+        print(json.dumps({"P": P, "T": T, "drop": drop, "bits": bits, **run(P, T, 12, drop, bits=bits)}),
+              flush=True)
