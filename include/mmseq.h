@@ -105,23 +105,23 @@ mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int64_t lda, c
 mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, void* out, int64_t ld_out, float* lse,
-                            mmseq_dtype dtype, const mmseq_dropout* drop, mmseq_stream stream);
+                            mmseq_dtype dtype, const mmseq_dropout* drop, uint64_t* keep_bits,
+                            mmseq_stream stream);
 mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, const void* out, int64_t ld_out, const void* dout,
                             int64_t ld_dout, const float* lse, float* delta, void* dqkv,
                             int64_t ld_dqkv, mmseq_dtype dtype, const mmseq_dropout* drop,
-                            uint64_t* keep_bits, mmseq_stream stream);
+                            const uint64_t* keep_bits, mmseq_stream stream);
 /* bf16 attention kernel selection: 1 (default) = 128-row workgroups with LDS-DMA double-buffered
  * K/V (or Q/dO) tiles and the delta = rowsum(dO * O) reduction fused into the dQ kernel;
  * 0 = 64-row register-staged kernels (cross-check in the tests). fp32 always uses the latter. */
 void mmseq_attn_set_fast(int enable);
-/* Attention-probability dropout in the bf16 backward: with a keep_bits workspace (uninitialised,
- * mmseq_attn_keep_bits_words() uint64 words) the dQ kernel, which regenerates the counter-based
- * mask anyway, also stores it as bits (word [(p*heads + h)*T + q][kt] for key tile kt <
- * round_up_even(ceil(T/64)); key 64*kt + j at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3)),
- * and the dK/dV kernel reads them instead of hashing every (query, key) element again; NULL
- * regenerates the mask in both. Size in uint64 words: */
+/* Attention-probability dropout keep-mask cache (bf16 fast kernels): with keep_bits != NULL the
+ * forward also stores its counter-based keep mask as bits (word [(p*heads + h)*T + q][kt] for key
+ * tile kt < round_up_even(ceil(T/64)); key 64*kt + j at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 +
+ * (j & 3)) and the backward, given the same buffer, reads them instead of hashing every
+ * (query, key) element again; NULL in both regenerates the mask. Size in uint64 words: */
 int64_t mmseq_attn_keep_bits_words(int P, int T, int heads);
 
 /* Small multi-head attention for the BERSON inter-sentence encoder (neural.py:98-235):

@@ -67,7 +67,7 @@ _SIGS = {
     "mmseq_gemm_set_workspace": (None, [_vp, _c_i64]),
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
-                                                           ctypes.c_int, _dp, _vp]),
+                                                           ctypes.c_int, _dp, _vp, _vp]),
     "mmseq_attn_keep_bits_words": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
@@ -216,15 +216,15 @@ def attn_set_fast(enable):
 
 
 def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse,
-             drop=None):
+             drop=None, keep_bits=None):
     _dev(qkv, out, lse)
     _check(lib().mmseq_attn_fwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
-                                scale, _p(out), ld_out, _p(lse), dt(qkv), _d(drop), _stream()),
-           "mmseq_attn_fwd")
+                                scale, _p(out), ld_out, _p(lse), dt(qkv), _d(drop), _p(keep_bits),
+                                _stream()), "mmseq_attn_fwd")
 
 
 def attn_keep_bits(P, T, heads, device):
-    """Backward workspace for the attention-dropout keep mask as bits (dQ writes, dK/dV reads)."""
+    """Buffer for the forward's attention-dropout keep mask as bits (read back by attn_bwd)."""
     return torch.empty(lib().mmseq_attn_keep_bits_words(P, T, heads), dtype=torch.int64,
                        device=device)
 

@@ -544,6 +544,11 @@ __device__ __forceinline__ bf16x8_t lds_tr(const unsigned short* img, int off) {
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, v);
 }
+// Consume register loads before the tile loop: the compiler then places its vmcnt wait for them
+// here, once, rather than at their first use inside the loop (where, since vmcnt retires in
+// order, it would also wait out that iteration's in-flight K/V prefetch).
+template <typename V>
+__device__ __forceinline__ void settle(const V& v) { asm volatile("" ::"v"(v)); }
 __device__ __forceinline__ f32x4 mma(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -570,8 +575,8 @@ __device__ __forceinline__ BlkIdx attn_block(int nx, int heads) {
 }
 
 // ---- forward ---------------------------------------------------------------------------------
-template <int DMODE>  // dropout: 0 none, 1 counter hash
-__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
+template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep bits out
+__global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
   float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
@@ -588,6 +593,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
   const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
   const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
   const uint32_t loff = dma_lane_off(lane, ld);
+  // keep-bit slices (DMODE 2): ushort g of word [q][t] of this (p, h), byte offset from its base
+  const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + ((int64_t)p * a.heads + h) * T * a.nkt2,
+                                              (int64_t)T * a.nkt2 * 8)
+                                  : make_rsrc(a.qkv, 0);
+  const uint32_t boff0 = (uint32_t)(((qw + i) * a.nkt2 * 4 + g) * 2);
   auto stage = [&](int t) {
     unsigned short* kimg = smem + (t & 1) * 2 * IMG;
 #pragma unroll
@@ -608,7 +618,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[grp][ks] = glob_row_frag(Qb, ld, qw + grp * 16 + i, T, ks, lane);
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[grp][ks] = glob_row_frag(Qb, ld, qw + grp * 16 + i, T, ks, lane);
+      settle(qf[grp][ks]);
+    }
 
   const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
   int to[4];
@@ -629,8 +642,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
     for (int d = 0; d < 4; ++d) o[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   for (int t = 0; t < nkt; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile t landed everywhere; buffer (t + 1) & 1 no longer read
+    // vmcnt retires in issue order: an active wave's two keep-bit stores of tile t - 1 are newer
+    // than tile t's DMA, so waiting down to 2 covers the DMA without waiting for the store acks
+    // (a raw s_barrier: __syncthreads' fence would add a vmcnt(0) for the stores)
+    if (DMODE == 2 && active && t > 0)
+      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // tile t landed everywhere; buffer (t + 1) & 1 no longer read
     if (t + 1 < nkt) stage(t + 1);
     if (!active) continue;
     const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
@@ -679,13 +698,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
 #pragma unroll
       for (int d = 0; d < 4; ++d) o[grp][d] *= alpha;
       if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax)
+        uint32_t kb16 = 0;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
           float dm[4];
           drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[grp][kb][r] *= dm[r];
+          for (int r = 0; r < 4; ++r) {
+            s[grp][kb][r] *= dm[r];
+            if (DMODE == 2) kb16 |= (dm[r] != 0.f ? 1u : 0u) << (kb * 4 + r);
+          }
         }
+        if (DMODE == 2)  // rows q >= T fall outside the descriptor and are dropped
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)kb16, rbits,
+                                                    boff0 + grp * 16 * a.nkt2 * 8 + t * 8, 0, 0);
       }
       pf[grp][0] = pack_pair(s[grp][0], s[grp][1]);
       pf[grp][1] = pack_pair(s[grp][2], s[grp][3]);
@@ -720,7 +746,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(AttnArgs a) {
 }
 
 // ---- backward: dQ (per 128-query block, keys swept), also writes delta = rowsum(dO * O) --------
-template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep-bit words for dK/dV
+template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
 __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
@@ -738,6 +764,11 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
   const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
   const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
   const uint32_t loff = dma_lane_off(lane, ld);
+  // keep-bit slices (DMODE 2) written by the forward; rows q >= T read as zero
+  const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + ((int64_t)p * a.heads + h) * T * a.nkt2,
+                                              (int64_t)T * a.nkt2 * 8)
+                                  : make_rsrc(a.qkv, 0);
+  const uint32_t boff0 = (uint32_t)(((qw + i) * a.nkt2 * 4 + g) * 2);
   auto stage = [&](int t) {
     unsigned short* kimg = smem + (t & 1) * 2 * IMG;
 #pragma unroll
@@ -779,6 +810,9 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     const int64_t ri = ((int64_t)p * a.heads + h) * T + q;
     L2[grp] = q < T ? a.lse[ri] * LOG2E : 1e30f;
     if (q < T && g == 0) a.delta[ri] = dot;
+    settle(qf[grp][0]);
+    settle(qf[grp][1]);
+    settle(L2[grp]);
   }
   const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
   int to[4];
@@ -796,10 +830,27 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) dq[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  uint32_t kwn[2] = {0xFFFFu, 0xFFFFu};  // keep slices of the next tile (DMODE 2)
+  if (DMODE == 2 && active) {
+#pragma unroll
+    for (int grp = 0; grp < 2; ++grp)
+      kwn[grp] = __builtin_amdgcn_raw_buffer_load_b16(rbits, boff0 + grp * 16 * a.nkt2 * 8, 0, 0);
+  }
   for (int t = 0; t < nkt; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const uint32_t kw16[2] = {kwn[0], kwn[1]};
+    if (DMODE == 2) {  // landed with the wait above; settling here keeps the compiler's wait out
+      settle(kw16[0]);  // of the tile body (it would cover the prefetch DMA issued below)
+      settle(kw16[1]);
+    }
     if (t + 1 < nkt) stage(t + 1);
+    if (DMODE == 2 && active) {  // keep slices of tile t + 1, consumed next round (past the last
+                                 // tile this reads the next row's word or, at the end, zero)
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp)
+        kwn[grp] = __builtin_amdgcn_raw_buffer_load_b16(rbits, boff0 + grp * 16 * a.nkt2 * 8 + (t + 1) * 8, 0, 0);
+    }
     if (!active) continue;
     const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* vimg = kimg + IMG;
@@ -821,16 +872,15 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     for (int kb = 0; kb < 4; ++kb)
       bias[kb] = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 16 + 4 * g);
     bf16x8_t dsf[2][2];
-    uint32_t kb16[2] = {0u, 0u};  // keep bits: 16-bit slice g of the tile word, bit kb*4 + r
 #pragma unroll
     for (int grp = 0; grp < 2; ++grp) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         float dm[4] = {1.f, 1.f, 1.f, 1.f};
-        if (DROP) drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
+        if (DMODE == 1) drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
         if (DMODE == 2) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) kb16[grp] |= (dm[r] != 0.f ? 1u : 0u) << (kb * 4 + r);
+          for (int r = 0; r < 4; ++r) dm[r] = ((kw16[grp] >> (kb * 4 + r)) & 1u) ? a.drop.scale : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -840,12 +890,6 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
       }
       dsf[grp][0] = pack_pair(dp[grp][0], dp[grp][1]);
       dsf[grp][1] = pack_pair(dp[grp][2], dp[grp][3]);
-      if (DMODE == 2) {
-        const int q = qw + grp * 16 + i;
-        if (q < T)
-          reinterpret_cast<unsigned short*>(a.bits)[((((int64_t)p * a.heads + h) * T + q) * a.nkt2 + t) * 4 + g] =
-              (unsigned short)kb16[grp];
-      }
     }
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -872,7 +916,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
 }
 
 // ---- backward: dK, dV (per 128-key block, queries swept; key on the MFMA lane) ----------------
-template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep-bit words from the dQ kernel
+template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
 __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (Q, dO) + lse, D
@@ -931,6 +975,12 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
       vf[grp][ks] = glob_row_frag(Vb, ld, key, T, ks, lane);
     }
     kb2[grp] = key < T ? (kbias ? kbias[key] * LOG2E : 0.f) : -1e30f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      settle(kf[grp][ks]);
+      settle(vf[grp][ks]);
+    }
+    settle(kb2[grp]);
   }
   const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
   int to[4];
@@ -1082,7 +1132,8 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
                                        int64_t q_off, int64_t k_off, int64_t v_off,
                                        const float* key_bias, float scale, void* out,
                                        int64_t ld_out, float* lse, mmseq_dtype dtype,
-                                       const mmseq_dropout* drop, mmseq_stream stream) {
+                                       const mmseq_dropout* drop, uint64_t* keep_bits,
+                                       mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   MMSEQ_REQUIRE(out && lse && ld_out >= heads * 64, "attn_fwd: bad out/lse");
@@ -1098,7 +1149,12 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4;
-    if (a.drop.thr)
+    a.nkt2 = (((T + 63) / 64) + 1) & ~1;
+    a.bits = keep_bits;
+    a.nkt2 = (((T + 63) / 64) + 1) & ~1;
+    if (a.drop.thr && keep_bits)
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel<2>, gq, dim3(256), lds, s, a);
+    else if (a.drop.thr)
       hipLaunchKernelGGL(attn_fwd_bf16_kernel<1>, gq, dim3(256), lds, s, a);
     else
       hipLaunchKernelGGL(attn_fwd_bf16_kernel<0>, gq, dim3(256), lds, s, a);
@@ -1115,7 +1171,7 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
                                        int64_t ld_out, const void* dout, int64_t ld_dout,
                                        const float* lse, float* delta, void* dqkv,
                                        int64_t ld_dqkv, mmseq_dtype dtype,
-                                       const mmseq_dropout* drop, uint64_t* keep_bits,
+                                       const mmseq_dropout* drop, const uint64_t* keep_bits,
                                        mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
@@ -1139,7 +1195,7 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
                   "attn_bwd: out / dqkv must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2 + 2048;
-    a.bits = keep_bits;
+    a.bits = const_cast<uint64_t*>(keep_bits);
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
     if (a.drop.thr && keep_bits) {
       hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gq, dim3(256), lds, s, a);

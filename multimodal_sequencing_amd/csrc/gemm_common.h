@@ -84,8 +84,17 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
 }
 
+// 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... lds; destination M0 + 16 * lane), issued
+// as inline asm on purpose: the compiler's waitcnt pass cannot tell an in-flight DMA into one LDS
+// buffer from a ds_read_b64_tr_b16 of the other and puts a vmcnt(0) in front of every transposed
+// read, which waits out the next tile's prefetch in the middle of the current one. Every reader of
+// DMA'd data therefore waits explicitly (counted s_waitcnt vmcnt + s_barrier), which the kernels
+// do anyway. m0 is a reserved register that the compiler only materialises right before its own
+// m0 readers; none are left in these kernels (tests/test_structure.py audits the code object).
 __device__ __forceinline__ void dma16(rsrc_t r, unsigned short* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (MMSEQ_LDS void*)lds, 16, voff, 0, 0, 0);
+  const uint32_t la = (uint32_t)(uintptr_t)lds;  // low 32 bits of an LDS-aperture address
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(la)), "v"(voff), "s"(r) : "memory");
 }
 
 

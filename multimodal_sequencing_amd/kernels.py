@@ -107,8 +107,10 @@ class BertLayerFn(torch.autograd.Function):
         qkv = _linear(x, Wqkv, bias=bqkv)
         o = torch.empty_like(x)
         lse = torch.empty(P, heads, T, device=x.device)
+        # the forward's dropout keep mask as bits (1 bit per score; read back by the backward)
+        kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None else None
         N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
-                   H, lse, drop=d_att)
+                   H, lse, drop=d_att, keep_bits=kbits)
         s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, drop=d_o)
         h1 = torch.empty_like(x)
         m1 = torch.empty(s1.shape[0], device=x.device)
@@ -125,6 +127,7 @@ class BertLayerFn(torch.autograd.Function):
                         _rows(H), m2, r2)
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
         ctx.meta = (L, P, T, heads, drops)
+        ctx.kbits = kbits
         return y
 
     @staticmethod
@@ -158,11 +161,9 @@ class BertLayerFn(torch.autograd.Function):
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
-        # dropout keep mask as bits: written by the dQ kernel, read by the dK/dV kernel
-        kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None else None
         N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
-                   H, do, H, lse, delta, dqkv, 3 * H, drop=d_att, keep_bits=kbits)
-        del kbits
+                   H, do, H, lse, delta, dqkv, 3 * H, drop=d_att, keep_bits=ctx.kbits)
+        ctx.kbits = None
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None

@@ -119,7 +119,7 @@ def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked, bits):
     out = torch.empty(P * T, H, device=DEV, dtype=dtype)
     lse = torch.empty(P, heads, T, device=DEV)
     kb = nat.attn_keep_bits(P, T, heads, DEV) if bits else None
-    nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse, drop=d)
+    nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse, drop=d, keep_bits=kb)
     Tp2 = (T + 1) & ~1  # attention mask rows are laid out with an even stride
     Mk = _mask((P, heads, T, Tp2), d)[..., :T]
     qf = qkv.float().requires_grad_(True)

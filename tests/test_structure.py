@@ -54,3 +54,36 @@ def test_abi_exports_every_declared_symbol():
         n = 0 if args.strip() in ("void", "") else len(args.split(","))
         assert len(_native._SIGS[name][1]) == n, name
     assert lib.mmseq_version().startswith(b"mmseq")
+
+
+def test_code_object_m0_only_feeds_lds_dma():
+    """The LDS-DMA helper (csrc/gemm_common.h dma16) writes m0 from inline asm, which the compiler
+    does not track: check in the built gfx950 code object that every m0 write is that helper's
+    `s_mov_b32 m0, sN` directly followed by its `buffer_load_dwordx4 ... lds`, and that nothing
+    compiler-generated reads m0 (indexed moves, messages, GWS, interpolation)."""
+    import shutil
+    import subprocess
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not (shutil.which("objcopy") and os.path.exists(os.path.join(llvm, "llvm-objdump"))):
+        pytest.skip("objcopy / ROCm llvm tools not available")
+    so = os.path.join(ROOT, "multimodal_sequencing_amd", "_lib", "libmmseq.so")
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", so], check=True)
+        subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--type=o", f"--input={fb}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}", "--unbundle"],
+                       check=True)
+        asm = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", "--mcpu=gfx950", co],
+                             check=True, capture_output=True, text=True).stdout
+    lines = [l.split("//")[0].strip() for l in asm.splitlines()]
+    lines = [l for l in lines if l and not l.endswith(">:")]
+    writes = 0
+    for k, l in enumerate(lines):
+        if re.search(r"\bm0\b", l):
+            assert re.fullmatch(r"s_mov_b32 m0, s\d+", l), l
+            assert lines[k + 1].startswith("buffer_load_dwordx4") and lines[k + 1].endswith("lds"), \
+                lines[k + 1]
+            writes += 1
+        assert not re.match(r"(s_movrel|v_movrel|s_sendmsg|ds_gws|s_set_gpr_idx|v_interp)", l), l
+    assert writes > 0

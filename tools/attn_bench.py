@@ -17,7 +17,8 @@ def run(P, T, heads, drop, iters=5, bits=False):
     dqkv = torch.empty_like(qkv)
     d = N.drop(0.1, 5, 99) if drop else None
     kb = N.attn_keep_bits(P, T, heads, "cuda") if bits else None
-    fwd = lambda: N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, lse, drop=d)
+    fwd = lambda: N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, lse, drop=d,
+                             keep_bits=kb)
     bwd = lambda: N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, dout, H,
                              lse, delta, dqkv, 3 * H, drop=d, keep_bits=kb)
     res = {}
