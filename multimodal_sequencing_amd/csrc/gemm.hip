@@ -15,6 +15,7 @@
 // for the fused epilogue (bias, activation / activation-backward, residual, accumulate).
 // Staging: global -> registers (16 B per lane per chunk, issued before the MFMA loop of the
 // previous tile) -> LDS after the barrier (the async-STAGE split of the guide, T14).
+#include <cstdlib>
 #include "gemm_common.h"
 
 static int g_disable_fast = 0;  // test hook: force the generic kernel
@@ -690,6 +691,11 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       g_num_cu = n;
+    // MMSEQ_GEMM_CUS: persistent-grid size override for measurement (tools/gemm_epi_bench.py)
+    if (const char* e = getenv("MMSEQ_GEMM_CUS")) {
+      const int v = atoi(e);
+      if (v > 0 && v <= g_num_cu) g_num_cu = v;
+    }
     cu_init = 1;
   }
   GemmArgs a;

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   const int G = gridDim.x;
   // XCD-aware order: the G/8 blocks sharing an XCD take consecutive tiles (shared A panels in L2)
   const int bid = blockIdx.x;
-  const int first = (G & 7) == 0 ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  const int first = xcd_item(bid, G);
   const int nk = a.K >> 6;
   const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
   const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
   const int wr = wave >> 2, wc = wave & 3;
   const int G = gridDim.x;
   const int bid = blockIdx.x;
-  const int item = (G & 7) == 0 ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  const int item = xcd_item(bid, G);
   const int split = item / ntiles, tile = item - split * ntiles;
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * 256, n0 = tn * 256;
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tile
   const int wr = wave >> 1, wc = wave & 1;
   const int G = gridDim.x;
   const int bid = blockIdx.x;
-  const int first = (G & 7) == 0 ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  const int first = xcd_item(bid, G);
   const int nk = a.K >> 5;  // 32-deep k-steps per tile
   const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
   const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);

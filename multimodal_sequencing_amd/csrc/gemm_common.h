@@ -84,6 +84,15 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
 }
 
+// XCD-aware work index: workgroups are dispatched round-robin over the 8 XCDs (block b on XCD
+// b & 7), so XCD x holds q + (x < r) of the G = 8q + r blocks; numbering each XCD's blocks
+// consecutively gives the ones that share operand panels (same K-split / neighbouring tiles)
+// one L2. A bijection on [0, G) for any G.
+__device__ __forceinline__ int xcd_item(int b, int G) {
+  const int q = G >> 3, r = G & 7, x = b & 7;
+  return x * q + min(x, r) + (b >> 3);
+}
+
 // 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... lds; destination M0 + 16 * lane), issued
 // as inline asm on purpose: the compiler's waitcnt pass cannot tell an in-flight DMA into one LDS
 // buffer from a ds_read_b64_tr_b16 of the other and puts a vmcnt(0) in front of every transposed
