@@ -42,31 +42,63 @@ __device__ __forceinline__ EpiIn epi8_load(const GemmArgs& a, int m, int n) {
   return in;
 }
 
+// Bias of a lane's 8 output columns n .. n + 7, loaded once per tile before any of its stores
+// (vmcnt retires loads and stores in issue order: a bias load inside each call would wait for
+// every store issued before it).
+struct EpiBias { f32x4 b0, b1; };
+__device__ __forceinline__ EpiBias epi_bias(const GemmArgs& a, int n) {
+  EpiBias b;
+  b.b0 = b.b1 = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (!a.bias || n >= a.N) return b;
+  if ((((uintptr_t)a.bias) & 15) == 0) {  // wave-uniform: two 16-byte loads
+    b.b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
+    b.b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { b.b0[r] = a.bias[n + r]; b.b1[r] = a.bias[n + 4 + r]; }
+  }
+  // consume here: otherwise the waitcnt state, merged over the per-call bounds branches, keeps
+  // the loads "pending" and puts a vmcnt(0) (= every earlier store) in front of each call
+  asm volatile("" ::"v"(b.b0), "v"(b.b1));
+  return b;
+}
+
 template <int ACT, bool BWD, bool XIN>
-__device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi, const EpiIn& in) {
+__device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi, const EpiIn& in,
+                                     const EpiBias& bias) {
   if (m >= a.M || n >= a.N) return;
   float v[8];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) { v[r] = lo[r] * a.alpha; v[4 + r] = hi[r] * a.alpha; }
-  if (a.bias) {
-    if ((((uintptr_t)a.bias) & 15) == 0) {  // wave-uniform: two 16-byte loads
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { v[r] += b0[r]; v[4 + r] += b1[r]; }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] += a.bias[n + r];
-    }
+  for (int r = 0; r < 4; ++r) {
+    v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
+    v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
   }
   const int64_t off = (int64_t)m * a.ldc + n;
   if (BWD) {
+    if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] *= act_bwd_fast(ACT, bf2f(in.x[r]));
+      for (int r = 0; r < 8; r += 2) {
+        const f32x2 d = gelu_bwd_pair((f32x2){bf2f(in.x[r]), bf2f(in.x[r + 1])});
+        v[r] *= d[0];
+        v[r + 1] *= d[1];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] *= act_bwd_fast(ACT, bf2f(in.x[r]));
+    }
   } else if (ACT) {
     if (a.aux) st8(reinterpret_cast<us*>(a.aux) + off, v);
+    if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
+      for (int r = 0; r < 8; r += 2) {
+        const f32x2 y = gelu_fwd_pair((f32x2){v[r], v[r + 1]});
+        v[r] = y[0];
+        v[r + 1] = y[1];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
+    }
   }
   if (a.drop.thr) {  // m * N + n is even (N % 8 == 0, n % 8 == 0): one hash per pair
     float dm[8];
@@ -297,21 +329,36 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
       continue;
     }
-    if (XIN) {  // batches of 4 calls: the operand loads of a batch are issued together
+    const EpiBias bias0 = epi_bias(a, n0 + wc * 64 + 8 * g), bias1 = epi_bias(a, n0 + wc * 64 + 32 + 8 * g);
+    if (XIN) {
+      // batches of 4 calls; the operand loads of batch h + 1 are issued before the stores of batch
+      // h, and each batch is consumed (settled) once, so its wait never covers a store (vmcnt
+      // retires in issue order; a consume inside the per-call bounds branches would wait vmcnt(0))
+      EpiIn in[2][2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          in[0][i][t] = epi8_load<BWD>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        EpiIn in[2][2];
+        if (h + 1 < 4) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-            in[i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
+            for (int t = 0; t < 2; ++t)
+              in[(h + 1) & 1][i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + 2 + i) * 16 + ii,
+                                                     n0 + wc * 64 + 32 * t + 8 * g);
+        }
+        asm volatile("" ::"v"(in[h & 1][0][0].x), "v"(in[h & 1][0][1].x), "v"(in[h & 1][1][0].x),
+                     "v"(in[h & 1][1][1].x));
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int t = 0; t < 2; ++t)
             epi8<ACT, BWD, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[i][t]);
+                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
+                                 t ? bias1 : bias0);
       }
     } else {
       const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
@@ -320,7 +367,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
 #pragma unroll
         for (int t = 0; t < 2; ++t)
           epi8<ACT, BWD, false>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                acc[i][2 * t], acc[i][2 * t + 1], none);
+                                acc[i][2 * t], acc[i][2 * t + 1], none, t ? bias1 : bias0);
     }
   }
 #undef FR
@@ -615,21 +662,36 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tile
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
     const int m0 = tm * 256, n0 = tn * 128;
     const int ii = lane & 15;
-    if (XIN) {  // batches of 4 calls: the operand loads of a batch are issued together
+    const EpiBias bias0 = epi_bias(a, n0 + wc * 64 + 8 * g), bias1 = epi_bias(a, n0 + wc * 64 + 32 + 8 * g);
+    if (XIN) {
+      // batches of 4 calls; the operand loads of batch h + 1 are issued before the stores of batch
+      // h, and each batch is consumed (settled) once, so its wait never covers a store (vmcnt
+      // retires in issue order; a consume inside the per-call bounds branches would wait vmcnt(0))
+      EpiIn in[2][2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          in[0][i][t] = epi8_load<BWD>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        EpiIn in[2][2];
+        if (h + 1 < 4) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-            in[i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
+            for (int t = 0; t < 2; ++t)
+              in[(h + 1) & 1][i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + 2 + i) * 16 + ii,
+                                                     n0 + wc * 64 + 32 * t + 8 * g);
+        }
+        asm volatile("" ::"v"(in[h & 1][0][0].x), "v"(in[h & 1][0][1].x), "v"(in[h & 1][1][0].x),
+                     "v"(in[h & 1][1][1].x));
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int t = 0; t < 2; ++t)
             epi8<ACT, BWD, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[i][t]);
+                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
+                                 t ? bias1 : bias0);
       }
     } else {
       const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
@@ -638,7 +700,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tile
 #pragma unroll
         for (int t = 0; t < 2; ++t)
           epi8<ACT, BWD, false>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                acc[i][2 * t], acc[i][2 * t + 1], none);
+                                acc[i][2 * t], acc[i][2 * t + 1], none, t ? bias1 : bias0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
