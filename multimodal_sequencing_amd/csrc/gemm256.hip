@@ -548,20 +548,45 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
   }
   float* C = a.splitk > 1 ? a.slab + (int64_t)split * a.M * a.N : reinterpret_cast<float*>(a.C);
   const int64_t ldc = a.splitk > 1 ? a.N : a.ldc;
-  const bool acc_c = a.splitk == 1 && a.accumulate;
+  // Two loops on the uniform accumulate flag: a C load anywhere in the store loop would put a
+  // vmcnt(0) (= every earlier store, in-order retirement) in front of each store. Accumulate: the
+  // C rows of i-step i + 1 are loaded before the stores of step i and consumed once per step.
+  if (!(a.splitk == 1 && a.accumulate)) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wr * 128 + i * 16 + ii;
+        const int n = n0 + wc * 64 + j * 16 + 4 * g;
+        if (m < a.M && n < a.N)  // N % 8 == 0: n .. n + 3 in range
+          *reinterpret_cast<f32x4*>(C + (int64_t)m * ldc + n) = acc[i][j];
+      }
+  } else {
+    auto ld = [&](int i, int j) {
       const int m = m0 + wr * 128 + i * 16 + ii;
       const int n = n0 + wc * 64 + j * 16 + 4 * g;
-      if (m < a.M && n < a.N) {  // N % 8 == 0: n .. n + 3 in range
-        f32x4* cp = reinterpret_cast<f32x4*>(C + (int64_t)m * ldc + n);
-        f32x4 v = acc[i][j];
-        if (acc_c) v += *cp;
-        *cp = v;
+      return (m < a.M && n < a.N) ? *reinterpret_cast<const f32x4*>(C + (int64_t)m * ldc + n)
+                                  : (f32x4){0.f, 0.f, 0.f, 0.f};
+    };
+    f32x4 cin[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cin[0][j] = ld(0, j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cin[(i + 1) & 1][j] = ld(i + 1, j);
+      }
+      asm volatile("" ::"v"(cin[i & 1][0]), "v"(cin[i & 1][1]), "v"(cin[i & 1][2]), "v"(cin[i & 1][3]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wr * 128 + i * 16 + ii;
+        const int n = n0 + wc * 64 + j * 16 + 4 * g;
+        if (m < a.M && n < a.N)
+          *reinterpret_cast<f32x4*>(C + (int64_t)m * ldc + n) = acc[i][j] + cin[i & 1][j];
       }
     }
+  }
 }
 
 
