@@ -11,6 +11,7 @@ Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
+import re
 import math
 import os
 import sys
@@ -103,7 +104,10 @@ def pmc_traffic(group="gemm256_nt"):
     summary (profiles/r*_pmc_traffic.json, made by tools/pmc_traffic.py: FETCH_SIZE x 2 +
     WRITE_SIZE, the gfx950 corrections of MI355X_MICROARCH.md), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    def order(f):  # r<round>_v<version>: numeric, so v10 sorts after v9
+        m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), key=order)
     if not files:
         return None, None
     try:
