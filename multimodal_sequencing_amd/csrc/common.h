@@ -198,7 +198,9 @@ __host__ inline Drop make_drop(const mmseq_dropout* d) {
   return r;
 }
 __device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t pair) {
-  uint32_t x = ((uint32_t)pair ^ d.k0) + (uint32_t)(pair >> 32) * d.k1;
+  // high word enters by xor + add (no multiply: pair indices here stay below 2^32, and the
+  // lowbias32 rounds below provide the diffusion)
+  uint32_t x = ((uint32_t)pair ^ d.k0) + ((uint32_t)(pair >> 32) ^ d.k1);
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
