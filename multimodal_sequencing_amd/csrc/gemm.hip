@@ -594,18 +594,28 @@ __global__ __launch_bounds__(256) void colsum_simple_kernel(int M, int K, const 
   out[m] += v;
 }
 
-// C[m][n] (+)= sum_s slab[s][m][n] for any N (element-wise; the generic split-K path)
-__global__ __launch_bounds__(256) void splitk_reduce1_kernel(int M, int N, int S, const float* __restrict__ slab,
-                                                             float* __restrict__ C, int64_t ldc,
-                                                             int accumulate) {
-  const int64_t total = (int64_t)M * N;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int m = e / N, n = e % N;
-    float v = slab[e];
-    for (int s = 1; s < S; ++s) v += slab[(int64_t)s * total + e];
-    float* cp = C + (int64_t)m * ldc + n;
-    if (accumulate) v += *cp;
-    *cp = v;
+// fp32 split-K with the full epilogue: v = sum_s slab[s][m][n .. n+3] in split order, then the
+// same epilogue4 the unsplit kernel applies (bias, activation / aux / act', dropout, residual,
+// accumulate), so splitting changes only the summation grouping of the dot products
+__global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs a, int S, const float* __restrict__ slab) {
+  const int n4 = (a.N + 3) >> 2;
+  const int64_t total = (int64_t)a.M * n4, MN = (int64_t)a.M * a.N;
+  float* C = reinterpret_cast<float*>(a.C);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t e = (int64_t)m * a.N + n + r;
+      float x = 0.f;
+      if (n + r < a.N) {
+        x = slab[e];
+        for (int q = 1; q < S; ++q) x += slab[q * MN + e];
+      }
+      v[r] = x;
+    }
+    epilogue4<float>(a, C, reinterpret_cast<const float*>(a.resid), reinterpret_cast<float*>(a.aux),
+                     reinterpret_cast<const float*>(a.dact), m, n, v, 0);
   }
 }
 
@@ -775,14 +785,14 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
       e = out_dtype == MMSEQ_BF16 ? launch_fast<unsigned short>(trans, a, batch, s)
                                   : launch_fast<float>(trans, a, batch, s);
     }
-  } else if (in_dtype == MMSEQ_F32 && out_dtype == MMSEQ_F32 && batch == 1 && g_slab && !bias &&
-             !act && !aux_out && !dact_aux && !resid && alpha == 1.0f && !a.drop.thr &&
-             ((M + 127) / 128) * ((N + 127) / 128) < 128 && K >= 2048) {
-    // skinny fp32 GEMMs with a long K (head weight gradients over all tokens): split K over
-    // the CUs, fp32 partial slabs, fixed-order reduction (bitwise reproducible)
+  } else if (in_dtype == MMSEQ_F32 && out_dtype == MMSEQ_F32 && batch == 1 && g_slab &&
+             ((M + 127) / 128) * ((N + 127) / 128) < 128 && K >= 256) {
+    // fp32 GEMMs with few output tiles (the BERSON head: M = 16-400 rows per story batch, and
+    // its weight gradients over all tokens): split K over the CUs, fp32 partial slabs, a
+    // fixed-order reduction that applies the epilogue (bitwise reproducible)
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     int S = (g_num_cu + tiles - 1) / tiles;
-    if (S > K / 512) S = K / 512;
+    if (S > K / 128) S = K / 128;
     while (S > 1 && (int64_t)S * M * N * 4 > g_slab_bytes) --S;
     a.splitk = S;
     a.kchunk = ((K + S - 1) / S + 31) / 32 * 32;
@@ -796,10 +806,9 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
         hipLaunchKernelGGL((gemm_kernel<float, float, false>), grid, dim3(NT_THREADS), 0, s, a);
       e = hipGetLastError();
       if (e == hipSuccess) {
-        const int64_t tot = (int64_t)M * N;
+        const int64_t tot = (int64_t)M * ((N + 3) / 4);
         const unsigned blocks = (unsigned)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096);
-        hipLaunchKernelGGL(splitk_reduce1_kernel, dim3(blocks), dim3(256), 0, s, M, N, a.splitk,
-                           g_slab, (float*)C, ldc, accumulate);
+        hipLaunchKernelGGL(splitk_epi_kernel, dim3(blocks), dim3(256), 0, s, a, a.splitk, g_slab);
         e = hipGetLastError();
       }
     } else {

@@ -503,6 +503,57 @@ def test_gemm_fp32_splitk(trans, M, N, K):
     assert err <= 1e-5 * math.sqrt(K) * (1 + ref.abs().max().item()) / 8, err
 
 
+@pytest.mark.parametrize("M,N,K", [(80, 768, 768), (16, 3072, 768), (80, 768, 3072), (400, 3080, 768),
+                                   (7, 36, 300)])
+@pytest.mark.parametrize("epi", ["bias_gelu_aux", "resid", "dact", "drop", "acc"])
+def test_gemm_fp32_splitk_epilogue(M, N, K, epi):
+    """fp32 GEMMs with few output tiles (the BERSON head) split K and apply the epilogue in the
+    ordered reduction: same results as the unfused ops, bitwise reproducible."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    B = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    R = torch.randn(M, N, generator=g).to(DEV)
+    z = (A.double() @ B.double().t())
+    outs = []
+    for _ in range(2):
+        C = R.clone() if epi == "acc" else torch.empty(M, N, device=DEV)
+        aux = torch.empty(M, N, device=DEV)
+        kw = {}
+        if epi == "bias_gelu_aux":
+            kw = dict(bias=bias, act=1, aux=aux)
+        elif epi == "resid":
+            kw = dict(bias=bias, resid=R)
+        elif epi == "dact":
+            kw = dict(act=1, dact=R)
+        elif epi == "drop":
+            kw = dict(bias=bias, drop=nat.drop(0.1, 11, 5))
+        elif epi == "acc":
+            kw = dict(accumulate=True)
+        nat.gemm(A, B, C, M, N, K, **kw)
+        outs.append((C, aux))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    C, aux = outs[0]
+    zb = z + bias.double()
+    if epi == "bias_gelu_aux":
+        ref = torch.nn.functional.gelu(zb)
+        torch.testing.assert_close(aux.double(), zb, rtol=1e-5, atol=1e-5)
+    elif epi == "resid":
+        ref = zb + R.double()
+    elif epi == "dact":
+        x = R.double().requires_grad_(True)
+        (gx,) = torch.autograd.grad(torch.nn.functional.gelu(x).sum(), x)
+        ref = z * gx
+    elif epi == "drop":
+        y = torch.empty(M, N, device=DEV)
+        nat.dropout(zb.float().contiguous(), y, nat.drop(0.1, 11, 5))  # same (seed, stream, index)
+        ref = y.double()
+    else:
+        ref = z + R.double()
+    torch.testing.assert_close(C.double(), ref, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("M,N,K", [(768, 3072, 20000), (2304, 768, 4100), (768, 768, 164), (40, 96, 300),
                                    (3072, 768, 1000)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
