@@ -610,8 +610,14 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
   };
   stage(0);
   const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
-  for (int k = tid; k < nkt * 64; k += 256)
-    sBias[k] = k < T ? (kbias ? kbias[k] * LOG2E : 0.f) : -1e30f;
+  int* sZero = reinterpret_cast<int*>(sBias + nkt * 64);  // tile t's key bias is all zero
+  for (int tt = wave; tt < nkt; tt += 4) {
+    const int k = tt * 64 + lane;
+    const float bv = k < T ? (kbias ? kbias[k] * LOG2E : 0.f) : -1e30f;
+    sBias[k] = bv;
+    const bool z = __ballot(bv != 0.f) == 0;
+    if (lane == 0) sZero[tt] = z;
+  }
   const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
                              a.q_off + h * 64;
   bf16x8_t qf[2][2];
@@ -664,39 +670,72 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         s[grp][kb] = mma(k1, qf[grp][1], s[grp][kb]);
       }
     }
+    // all-zero key bias in this tile (the usual case: ViT, and every visual-key tile of the joint
+    // encoder): the scale folds into the exponent's FMA, no per-score bias add
+    // (not with dropout: the second code path costs the 3-waves-per-SIMD register budget there)
+    const bool zb = !DROP && __builtin_amdgcn_readfirstlane(sZero[t]) != 0;
     f32x4 bias[4];
+    if (!zb) {
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-      bias[kb] = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 16 + 4 * g);
+      for (int kb = 0; kb < 4; ++kb)
+        bias[kb] = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 16 + 4 * g);
+    }
     bf16x8_t pf[2][2];
 #pragma unroll
     for (int grp = 0; grp < 2; ++grp) {
       float mx = -1e30f;
+      if (zb) {
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = fmaf(s[grp][kb][r], c, bias[kb][r]);
-          s[grp][kb][r] = x;
-          mx = fmaxf(mx, x);
-        }
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[grp][kb][r]);
+        mx *= c;  // c > 0
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = fmaf(s[grp][kb][r], c, bias[kb][r]);
+            s[grp][kb][r] = x;
+            mx = fmaxf(mx, x);
+          }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[grp], mx);
-      const float alpha = ex2(m[grp] - mn);
-      m[grp] = mn;
+      // lazy rescaling: the running max only moves (and O, l are rescaled) when some row's tile
+      // max exceeds it by more than 8 (log2 units), so unrescaled probabilities stay <= 2^8;
+      // O / l and the LSE m + log2(l) are exact for any reference m
+      if (__ballot(mx > m[grp] + 8.f) != 0) {
+        const float mn = fmaxf(m[grp], mx);
+        const float alpha = ex2(m[grp] - mn);
+        m[grp] = mn;
+        l[grp] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[grp][d] *= alpha;
+      }
+      const float mn = m[grp];
       float rs = 0.f;
+      if (zb) {
+        const float nm = -mn;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = ex2(s[grp][kb][r] - mn);
-          s[grp][kb][r] = e;
-          rs += e;
-        }
-      l[grp] = fmaf(l[grp], alpha, rs);
+          for (int r = 0; r < 4; ++r) {
+            const float e = ex2(fmaf(s[grp][kb][r], c, nm));
+            s[grp][kb][r] = e;
+            rs += e;
+          }
+      } else {
 #pragma unroll
-      for (int d = 0; d < 4; ++d) o[grp][d] *= alpha;
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = ex2(s[grp][kb][r] - mn);
+            s[grp][kb][r] = e;
+            rs += e;
+          }
+      }
+      l[grp] += rs;
       if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax)
         uint32_t kb16 = 0;
 #pragma unroll
@@ -1148,8 +1187,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   if (dtype == MMSEQ_BF16 && g_attn_fast) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
-    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4;
-    a.nkt2 = (((T + 63) / 64) + 1) & ~1;
+    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;
     a.bits = keep_bits;
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
     if (a.drop.thr && keep_bits)
