@@ -1046,22 +1046,21 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     if (DMODE == 2) {
       // word (kt0 + (wave >> 1)) of a row holds this wave's keys; key j (0..63 in its tile) sits
       // at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3) (16-bit slice per forward lane group)
+      // With j = (wave & 1) * 32 + grp * 16 + i that bit is in dword (i >> 3) & 1 of the word at
+      // position ((i >> 2) & 1) * 16 + ((wave & 1) * 2 + grp) * 4 + (i & 3): one 32-bit LDS read
+      // per query serves both groups, one bit-field extract per element
       keep = 0;
-      const uint64_t* bw = reinterpret_cast<const uint64_t*>(sBits + (t & 1) * 512) + (wave >> 1);
-      int pos[2];
-#pragma unroll
-      for (int grp = 0; grp < 2; ++grp) {
-        const int j = (wave & 1) * 32 + grp * 16 + i;
-        pos[grp] = ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3);
-      }
+      const uint32_t* bw = reinterpret_cast<const uint32_t*>(sBits + (t & 1) * 512) +
+                           (wave >> 1) * 2 + ((i >> 3) & 1);
+      const uint32_t pos0 = ((i >> 2) & 1) * 16 + (wave & 1) * 8 + (i & 3);
 #pragma unroll
       for (int qs = 0; qs < 4; ++qs)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const uint64_t w = bw[(qs * 16 + 4 * g + r) * 2];
+          const uint32_t w = bw[(qs * 16 + 4 * g + r) * 4];
 #pragma unroll
           for (int grp = 0; grp < 2; ++grp)
-            keep |= (uint32_t)((w >> pos[grp]) & 1u) << (grp * 16 + qs * 4 + r);
+            keep |= __builtin_amdgcn_ubfe(w, pos0 + 4 * grp, 1) << (grp * 16 + qs * 4 + r);
         }
     }
     if (DMODE == 1) {
