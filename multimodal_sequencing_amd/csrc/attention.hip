@@ -672,8 +672,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
     }
     // all-zero key bias in this tile (the usual case: ViT, and every visual-key tile of the joint
     // encoder): the scale folds into the exponent's FMA, no per-score bias add
-    // (not with dropout: the second code path costs the 3-waves-per-SIMD register budget there)
-    const bool zb = !DROP && __builtin_amdgcn_readfirstlane(sZero[t]) != 0;
+    const bool zb = __builtin_amdgcn_readfirstlane(sZero[t]) != 0;
     f32x4 bias[4];
     if (!zb) {
 #pragma unroll
@@ -736,16 +735,23 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
           }
       }
       l[grp] += rs;
-      if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax)
+      if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax);
+                   // dropped scores are zeroed here, the 1/(1-p) of the kept ones is applied with
+                   // the final normalisation (one integer compare feeds select and keep bit)
         uint32_t kb16 = 0;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
-          float dm[4];
-          drop_mul_pairs<2>(a.drop, drow[grp] + t * 64 + kb * 16 + 4 * g, dm);
+          const uint64_t pr = (drow[grp] + t * 64 + kb * 16 + 4 * g) >> 1;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s[grp][kb][r] *= dm[r];
-            if (DMODE == 2) kb16 |= (dm[r] != 0.f ? 1u : 0u) << (kb * 4 + r);
+          for (int q2 = 0; q2 < 2; ++q2) {
+            const uint32_t h = drop_hash(a.drop, pr + q2);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              const int r = 2 * q2 + hf;
+              const bool keep = (hf ? (h >> 16) : (h & 0xFFFFu)) >= a.drop.thr;
+              s[grp][kb][r] = keep ? s[grp][kb][r] : 0.f;
+              if (DMODE == 2) kb16 |= (keep ? 1u : 0u) << (kb * 4 + r);
+            }
           }
         }
         if (DMODE == 2)  // rows q >= T fall outside the descriptor and are dropped
@@ -774,7 +780,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
     lt += __shfl_xor(lt, 32, 64);
     const int q = qw + grp * 16 + i;
     if (q < T) {
-      const float inv = 1.0f / lt;
+      const float inv = (DROP ? a.drop.scale : 1.0f) / lt;
       unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
                            h * 64 + 4 * g;
 #pragma unroll
