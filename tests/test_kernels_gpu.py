@@ -175,6 +175,58 @@ def test_attention_fwd_bwd(dtype, P, T, heads, masked, fast):
     nat.attn_set_fast(1)
 
 
+@pytest.mark.parametrize("profile", ["ramp_up", "ramp_down", "jump"])
+@pytest.mark.parametrize("bias_mode", ["none", "first_tile_masked", "zeros"])
+def test_attention_rescale_and_zero_bias_tiles(profile, bias_mode):
+    """bf16 fast kernels: the running max moves only when a row's tile max exceeds it by > 8
+    (log2) and all-zero-bias key tiles skip the bias add. Scores that climb across key tiles
+    (several rescales mid-sequence), fall (none after the first tile) or jump, with a key bias
+    masked only inside the first tile (later tiles take the zero-bias path)."""
+    P, T, heads = 2, 300, 2
+    H = heads * 64
+    g = torch.Generator(device="cpu").manual_seed(11)
+    q, k, v = (torch.randn(3, P, T, heads, 64, generator=g) * 0.3).unbind(0)
+    u = torch.nn.functional.normalize(torch.randn(64, generator=g), dim=0)
+    pos = torch.arange(T, dtype=torch.float32) / T
+    # score(q, key) ~ amp(key) * scale: ramps spanning ~54 log2 units (several rescales) and a
+    # jump of ~36 log2 units at key 200
+    if profile == "ramp_up":
+        amp = 300.0 * pos
+    elif profile == "ramp_down":
+        amp = 300.0 * (1 - pos)
+    else:
+        amp = torch.where(torch.arange(T) >= 200, 200.0, 0.0)
+    q = q + 3.0 * u
+    k = k + amp[None, :, None, None] * u / 3.0
+    qkv = torch.stack([q, k, v], 2).reshape(P * T, 3 * H).to(DEV, torch.bfloat16)
+    bias = None
+    if bias_mode == "first_tile_masked":
+        b = torch.zeros(P, T)
+        b[:, 10:20] = -10000.0
+        bias = b.to(DEV)
+    elif bias_mode == "zeros":
+        bias = torch.zeros(P, T, device=DEV)
+    scale = 1 / 8
+    out = torch.empty(P * T, H, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(P, heads, T, device=DEV)
+    nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse)
+    qf = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qf, P, T, heads, bias, scale)
+    _close(out, ref, torch.bfloat16)
+    qq, kk, _ = qkv.float().view(P, T, 3, heads, 64).unbind(2)
+    sc = torch.einsum("pqhd,pkhd->phqk", qq, kk) * scale
+    if bias is not None:
+        sc = sc + bias[:, None, None, :]
+    torch.testing.assert_close(lse, torch.logsumexp(sc, -1), rtol=1e-3, atol=1e-3)
+    dout = torch.randn(P * T, H, generator=g).to(DEV, torch.bfloat16)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(P, heads, T, device=DEV)
+    nat.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, dout, H, lse, delta,
+                 dqkv, 3 * H)
+    (ref_g,) = torch.autograd.grad(ref, qf, dout.float())
+    _close(dqkv, ref_g, torch.bfloat16, scale=2.0)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,cols,eps", [(100, 768, 1e-12), (7, 128, 1e-5), (300, 96, 1e-6)])
 def test_layernorm(dtype, rows, cols, eps):
