@@ -660,14 +660,22 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
     if (!active) continue;
     const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* vimg = kimg + IMG;
+    // 16-key blocks holding a valid key (the last tile of T = 64n + 1 has one): the others are
+    // all masked (p = 0), so their MFMAs and softmax work are skipped
+    const int nkb = t == nkt - 1 ? min(4, (T - t * 64 + 15) >> 4) : 4;
     f32x4 s[2][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      const bf16x8_t k0 = lds_row(kimg, kb * 1024 + ro0), k1 = lds_row(kimg, kb * 1024 + ro1);
+      if (kb < nkb) {
+        const bf16x8_t k0 = lds_row(kimg, kb * 1024 + ro0), k1 = lds_row(kimg, kb * 1024 + ro1);
 #pragma unroll
-      for (int grp = 0; grp < 2; ++grp) {
-        s[grp][kb] = mma(k0, qf[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
-        s[grp][kb] = mma(k1, qf[grp][1], s[grp][kb]);
+        for (int grp = 0; grp < 2; ++grp) {
+          s[grp][kb] = mma(k0, qf[grp][0], (f32x4){0.f, 0.f, 0.f, 0.f});
+          s[grp][kb] = mma(k1, qf[grp][1], s[grp][kb]);
+        }
+      } else {
+#pragma unroll
+        for (int grp = 0; grp < 2; ++grp) s[grp][kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     }
     // all-zero key bias in this tile (the usual case: ViT, and every visual-key tile of the joint
@@ -691,13 +699,15 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         mx *= c;  // c > 0
       } else {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb) {
+          if (kb >= nkb) continue;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float x = fmaf(s[grp][kb][r], c, bias[kb][r]);
             s[grp][kb][r] = x;
             mx = fmaxf(mx, x);
           }
+        }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -726,13 +736,18 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
           }
       } else {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb) {
+          if (kb >= nkb) {
+            s[grp][kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float e = ex2(s[grp][kb][r] - mn);
             s[grp][kb][r] = e;
             rs += e;
           }
+        }
       }
       l[grp] += rs;
       if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax);
@@ -741,6 +756,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         uint32_t kb16 = 0;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
+          if (kb >= nkb) continue;  // all keys >= T: p = 0, keep bits never read
           const uint64_t pr = (drow[grp] + t * 64 + kb * 16 + 4 * g) >> 1;
 #pragma unroll
           for (int q2 = 0; q2 < 2; ++q2) {
@@ -767,7 +783,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
 #pragma unroll
       for (int grp = 0; grp < 2; ++grp) {
         o[grp][d] = mma(v0, pf[grp][0], o[grp][d]);
-        o[grp][d] = mma(v1, pf[grp][1], o[grp][d]);
+        if (nkb > 2) o[grp][d] = mma(v1, pf[grp][1], o[grp][d]);
       }
     }
   }
