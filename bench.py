@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--micro", type=int, default=16, help="stories per micro-batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-timer", action="store_true")
+    ap.add_argument("--fwd-steps", type=int, default=3,
+                    help="forward-only passes timed after the training steps (north-star check)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,6 +209,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
 
+    # North-star forward check (stories/s_fwd x fwd FLOP/story / peak): the same
+    # batch, eval mode (no dropout), no autograd graph, timed like the training steps.
+    fwd_dt = None
+    if args.fwd_steps > 0:
+        model.eval()
+        with torch.no_grad():
+            for b in mbs:
+                model(b)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            f0 = time.perf_counter()
+            for _ in range(args.fwd_steps):
+                for b in mbs:
+                    model(b)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            fwd_dt = time.perf_counter() - f0
+        model.train()
+        if world > 1:
+            t = torch.tensor([fwd_dt], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            fwd_dt = t.item()
+
     Nst, per = preset["N"], preset["per_seq"]
     Pst = Nst * (Nst - 1)
     J = preset["joint"]
@@ -234,6 +263,13 @@ def main():
         "model_flops_util": stories / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
         "loss": float(loss.item()) if loss is not None else None,
     }
+    if fwd_dt is not None:
+        fst = args.batch * args.fwd_steps * world / fwd_dt
+        out["forward"] = {"stories_per_s": fst, "ms_per_batch": fwd_dt / args.fwd_steps * 1e3,
+                          "tflops": fst * fwd / 1e12,
+                          "mfma_frac": fst * fwd / 1e12 / PEAK_BF16_TFLOPS,
+                          "mode": "eval (no dropout), torch.no_grad, full model forward incl. "
+                                  "BERSON head + loss; ViT + joint encoder are >99.9% of FLOPs"}
     gs = timer.summary()
     if gs:
         traffic, tsrc = pmc_traffic()

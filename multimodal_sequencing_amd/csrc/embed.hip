@@ -183,6 +183,41 @@ __global__ __launch_bounds__(256) void im2col_kernel(int B, int N, int npair, in
   }
 }
 
+// bf16 patches: one row per 96 threads, 8 consecutive pixels of one (channel, patch row) per
+// thread (two 16-byte loads, one 16-byte store); the row's pair / image decode is done once
+// per row instead of per element (64-bit divisions). Requires ps % 8 == 0.
+__global__ __launch_bounds__(192) void im2col_bf16_kernel(int64_t rows, int N, int npair, int R,
+                                                         int ps, const float* __restrict__ images,
+                                                         const int64_t* __restrict__ pairs,
+                                                         unsigned short* __restrict__ out) {
+  const int g = R / ps, gg = g * g, K = 3 * ps * ps;
+  const int64_t row = (int64_t)blockIdx.x * 2 + threadIdx.x / 96;
+  const int chunk = threadIdx.x % 96;
+  if (row >= rows) return;
+  const int patch = (int)(row % gg);
+  const int64_t rest = row / gg;
+  const int s = (int)(rest & 1);
+  const int64_t pj = rest >> 1;
+  const int b = (int)(pj / npair);
+  const int img = (int)pairs[pj * 2 + s];
+  const int py = patch / g, px = patch % g;
+  const float* src_img = images + ((int64_t)b * N + img) * 3 * R * R;
+  for (int c8 = chunk; c8 * 8 < K; c8 += 96) {
+    const int col = c8 * 8;
+    const int c = col / (ps * ps), ky = (col / ps) % ps, kx = col % ps;
+    const float* src = src_img + ((int64_t)c * R + py * ps + ky) * R + px * ps + kx;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(src + 4);
+    u16x8 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[r] = f2bf(v0[r]);
+      o[4 + r] = f2bf(v1[r]);
+    }
+    *reinterpret_cast<u16x8*>(out + row * K + col) = o;
+  }
+}
+
 __device__ __forceinline__ int vit_pos_row(int t, int gg) {
   // clip/model.py:271-275 with img_len = 2: rows 0..gg for CLS + img0, rows 0..gg-1 for img1
   return t <= gg ? t : t - gg - 1;
@@ -420,7 +455,12 @@ extern "C" mmseq_status mmseq_vit_im2col(int B, int N, int npair, int R, int ps,
   if (dtype == MMSEQ_F32)
     hipLaunchKernelGGL(im2col_kernel<float>, grid, dim3(256), 0, s, B, N, npair, R, ps, images,
                        pairs, (float*)patches);
-  else
+  else if (ps % 8 == 0 && R % 4 == 0 && (((uintptr_t)images) & 15) == 0 &&
+           (((uintptr_t)patches) & 15) == 0) {
+    const int64_t rows = (int64_t)B * npair * 2 * (R / ps) * (R / ps);
+    hipLaunchKernelGGL(im2col_bf16_kernel, dim3((unsigned)((rows + 1) / 2)), dim3(192), 0, s, rows, N,
+                       npair, R, ps, images, pairs, (unsigned short*)patches);
+  } else
     hipLaunchKernelGGL(im2col_kernel<unsigned short>, grid, dim3(256), 0, s, B, N, npair, R, ps,
                        images, pairs, (unsigned short*)patches);
   return mmseq_check_launch("vit_im2col");
