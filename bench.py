@@ -4,10 +4,19 @@ pair sequence 512 (120 text + 393 ViT-B/16 tokens), BASELINE config 3 (1 GPU) / 
 One "step" = one optimizer step of the reference train loop (trainers/train.py:275-363) over a
 per-GPU batch of B stories (B = 32, config 3), all 20 ordered pairs per story, bf16 compute with
 fp32 master weights; synthetic seeded inputs already resident in HBM; random-init weights of the
-exact architecture. Launch (multi-GPU):
+exact architecture. Data parallel (config 4): one process per GPU, each rank takes its B stories
+of the global batch by the DistributedSampler rule (train.py:158-161), gradients are averaged by
+RCCL all-reduces issued from the layer backwards (trainer.GradAllReduce).
+
+`value` is the whole-job aggregate: per-GPU-batch training steps per second summed over the
+ranks, i.e. (stories/s over all GPUs) / B. With weak scaling (B fixed per GPU) the optimizer
+step rate is `optimizer_steps_per_s` (= value / n_gpus), reported beside it.
+
+Launch: `python bench.py --gpus N` re-launches itself under torch.distributed.run with N
+processes (before touching the GPU) when WORLD_SIZE is not set; the driver's form
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
-Rank 0 prints ONE JSON line.
+runs directly. Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -25,7 +34,8 @@ sys.path.insert(0, ROOT)
 
 from multimodal_sequencing_amd import _native as N  # noqa: E402
 from multimodal_sequencing_amd import model_zoo  # noqa: E402
-from multimodal_sequencing_amd.trainer import FusedAdamW, GradAllReduce, train_step  # noqa: E402
+from multimodal_sequencing_amd.trainer import (FusedAdamW, GradAllReduce,  # noqa: E402
+                                               distributed_indices, train_step)
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 
@@ -41,16 +51,27 @@ def story_flops(Pst, Lt, Tv, H, Lj, W, Lv, patch, E, ff=4):
     return Pst * (vit + visn + joint) + head
 
 
-def synthetic_batch(B, Nst, per_seq, vocab, res, device, seed):
-    g = torch.Generator(device="cpu").manual_seed(seed)
+def synthetic_story(idx, Nst, per_seq, vocab, res, seed):
+    """Story `idx` of the synthetic dataset: each step = <s>(0) + k ids
+    ~ U[3, vocab) + </s>(2), labels = argsort(randperm(N)), images ~ N(0, 1). A pure function of
+    (seed, idx), so any rank materialises exactly its own shard."""
+    g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + idx)
     k = per_seq - 2
-    content = torch.randint(3, vocab, (B, Nst, k), generator=g)
-    steps = torch.cat([torch.zeros(B, Nst, 1, dtype=torch.long), content,
-                       torch.full((B, Nst, 1), 2, dtype=torch.long)], -1)
-    ids = steps.view(B, Nst * per_seq)
-    labels = torch.stack([torch.argsort(torch.randperm(Nst, generator=g)) for _ in range(B)])
-    images = torch.randn(B, Nst, 3, res, res, generator=g).to(device)
-    return {"input_ids": ids, "labels": labels, "images": images}
+    content = torch.randint(3, vocab, (Nst, k), generator=g)
+    steps = torch.cat([torch.zeros(Nst, 1, dtype=torch.long), content,
+                       torch.full((Nst, 1), 2, dtype=torch.long)], -1)
+    labels = torch.argsort(torch.randperm(Nst, generator=g))
+    images = torch.randn(Nst, 3, res, res, generator=g)
+    return steps.view(Nst * per_seq), labels, images
+
+
+def synthetic_batch(B, Nst, per_seq, vocab, res, device, seed, indices=None):
+    """Batch of the stories `indices` (default 0..B-1) of the seeded synthetic dataset."""
+    indices = list(range(B)) if indices is None else list(indices)
+    ids, labels, images = zip(*(synthetic_story(i, Nst, per_seq, vocab, res, seed)
+                                for i in indices))
+    return {"input_ids": torch.stack(ids), "labels": torch.stack(labels),
+            "images": torch.stack(images).to(device)}
 
 
 class GemmTimer:
@@ -117,36 +138,76 @@ def pmc_traffic(group="gemm256_nt"):
         return None, None
 
 
-def cpu_baseline(preset, seconds_hint=30):
-    """The CPU oracle (fp32 PyTorch restatement, oracle/berson_oracle.py) timed on host cores:
-    one fwd+bwd of ONE story of the same config (bounded sample)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    from oracle import berson_oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    m = model_zoo.build_preset(preset, device="cpu", dtype=torch.float32)
-    params = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
-    p = model_zoo.PRESETS[preset]
-    data = synthetic_batch(1, p["N"], p["per_seq"], 50265, 224, "cpu", seed=7)
-    cfg = {"N": p["N"], "heads": p["joint"]["num_attention_heads"], "inter_heads": 8,
-           "text_only": p["vision"] is None, "vit_heads": None}
-    t0 = time.perf_counter()
-    loss, _, _ = O.forward_loss(params, data["input_ids"].numpy(), data["labels"].numpy(),
-                                data["images"], cfg)
-    loss.backward()
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
+def _physical_cores():
+    try:
+        import psutil
+        n = psutil.cpu_count(logical=False)
+        if n:
+            return n
+    except ImportError:
+        pass
+    return os.cpu_count() or 1
+
+
+def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": 1.0 / dt, "unit": "stories/s (fwd+bwd, fp32)", "cores": threads,
-            "kind": "port", "sample": f"1 story ({p['N']} steps, {p['N'] * (p['N'] - 1)} pairs) "
-            f"fwd+bwd of the oracle on {threads} threads of {cpu}; {dt:.1f} s"}
+    return "unknown"
+
+
+def cpu_baseline(preset, timed=3):
+    """The CPU oracle (fp32 PyTorch restatement, oracle/berson_oracle.py) on host cores, by the
+    BASELINE.md protocol: B = 1 story of the same config, eval mode, 1 warm-up, then the median
+    of `timed` fwd+bwd iterations, torch threads = physical cores (capped at this job's
+    16-CPU share of the box)."""
+    from oracle import berson_oracle as O
+    threads = max(1, min(16, _physical_cores()))
+    torch.set_num_threads(threads)
+    m = model_zoo.build_preset(preset, device="cpu", dtype=torch.float32)
+    p = model_zoo.PRESETS[preset]
+    data = synthetic_batch(1, p["N"], p["per_seq"], 50265, 224, "cpu", seed=7)
+    cfg = {"N": p["N"], "heads": p["joint"]["num_attention_heads"], "inter_heads": 8,
+           "text_only": p["vision"] is None, "vit_heads": None}
+    times = []
+    for it in range(1 + timed):
+        params = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+        t0 = time.perf_counter()
+        loss, _, _ = O.forward_loss(params, data["input_ids"].numpy(), data["labels"].numpy(),
+                                    data["images"], cfg)
+        loss.backward()
+        dt = time.perf_counter() - t0
+        print(f"[bench] cpu_baseline iteration {it} ({'warm-up' if it == 0 else 'timed'}): "
+              f"{dt:.1f} s", file=sys.stderr, flush=True)
+        if it > 0:
+            times.append(dt)
+    med = sorted(times)[len(times) // 2]
+    return {"value": 1.0 / med, "unit": "stories/s (fwd+bwd, fp32)", "cores": threads,
+            "kind": "port", "s_per_story": med,
+            "sample": f"1 story ({p['N']} steps, {p['N'] * (p['N'] - 1)} pairs) fwd+bwd of the "
+                      f"oracle, eval mode, 1 warm-up + median of {timed} "
+                      f"({', '.join(f'{t:.1f}' for t in times)} s) on {threads} threads "
+                      f"of {_cpu_model()}"}
+
+
+def _relaunch(args):
+    """`--gpus N` without a torchrun environment: start N ranks under torch.distributed.run as
+    a child process (nothing here has touched the GPU) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -161,25 +222,47 @@ def main():
     ap.add_argument("--no-gemm-timer", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=3,
                     help="forward-only passes timed after the training steps (north-star check)")
+    ap.add_argument("--bucket-mb", type=float, default=64.0,
+                    help="DP all-reduce bucket cap (MB of fp32 grads)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks "
+                         "sharing one GPU (RCCL refuses duplicate devices)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} GPUs (RCCL needs one GPU per rank)")
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+        assert dist.get_world_size() == args.gpus
 
     preset = model_zoo.PRESETS[args.config]
     model = model_zoo.build_preset(args.config, device=dev, dtype=torch.bfloat16, seed=0)
     model.train()  # dropout p = 0.1 at every reference site, counter-based masks
     model.bert.dropout_seed = 1 + rank
     stores = model.stores()
-    opt = FusedAdamW(stores, lr=5e-6, warmup=100)
-    reducer = GradAllReduce(stores) if world > 1 else None
+    # the reference's schedule: warmup 100 (wikihow_finetune.sh), t_total = the run length
+    opt = FusedAdamW(stores, lr=5e-6, warmup=100, total_steps=args.warmup + args.steps)
+    reducer = None
+    if world > 1:
+        units, begin = model.ddp_units()
+        reducer = GradAllReduce(stores, bucket_mb=args.bucket_mb, units=units, begin_units=begin)
+    # this rank's shard of the global batch (DistributedSampler rule over world * B stories)
+    shard = distributed_indices(args.batch * world, world, rank)
     data = synthetic_batch(args.batch, preset["N"], preset["per_seq"], 50265, 224, dev,
-                           seed=1000 + rank)
+                           seed=1000, indices=shard)
     mbs = []
     for o in range(0, args.batch, args.micro):
         mbs.append({k: v[o:o + args.micro] for k, v in data.items()})
@@ -249,7 +332,13 @@ def main():
     steps_s = args.steps * world / dt
     out = {
         "metric": "multimodal steps/sec (fwd+bwd) at N=5 steps, seq=512, ViT-B/16; 1/2/4/8 GPU",
-        "value": steps_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+        "value": steps_s, "unit": "steps/s",
+        "value_definition": f"aggregate {args.batch}-story per-GPU training steps (fwd+bwd+"
+                            "all-reduce+AdamW) per second summed over all GPUs = stories_per_s / "
+                            f"{args.batch}",
+        "optimizer_steps_per_s": args.steps / dt,
+        "n_gpus": world, "steps": args.steps,
+        "dist_backend": dist.get_backend() if world > 1 else None,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (seeded token ids U[3,50265), N(0,1) 224x224 images), random-init "
@@ -257,7 +346,10 @@ def main():
         "config": {"workload": f"{args.config}: ViT-B/16 + 12x768 joint encoder + BERSON, "
                                f"N={Nst} steps, {Pst} pairs/story, pair seq {Lt}+{Tv}={Lt + Tv}",
                    "global_batch": args.batch * world, "stories_per_gpu": args.batch,
-                   "micro_batch": args.micro, "seq_len": Lt + Tv, "parallelism": f"dp{world}"},
+                   "micro_batch": args.micro, "seq_len": Lt + Tv, "parallelism": f"dp{world}",
+                   "allreduce": (f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
+                                 f"mean all-reduce in <= {args.bucket_mb:g} MB buckets issued "
+                                 "from the layer backwards") if world > 1 else None},
         "stories_per_s": stories / dt,
         "model_tflops": stories / dt * 3 * fwd / 1e12,
         "model_flops_util": stories / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
@@ -273,6 +365,8 @@ def main():
     gs = timer.summary()
     if gs:
         traffic, tsrc = pmc_traffic()
+        if (args.config, args.batch, args.micro) != ("config3", 32, 16):
+            traffic, tsrc = None, None  # the committed PMC pass profiles the default workload
         out["roofline"] = {"bound": "mfma", "kernel": "gemm256_nt_kernel (bf16 NT: fwd + dgrad)",
                            "achieved": gs["achieved_tflops"], "peak": PEAK_BF16_TFLOPS,
                            "unit": "TFLOP/s", "frac": gs["achieved_tflops"] / PEAK_BF16_TFLOPS,

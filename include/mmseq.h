@@ -4,8 +4,11 @@
  *
  * C ABI: plain pointers and sizes, no torch types. Every entry point is stream-ordered on the
  * caller's hipStream_t, performs no host synchronisation and no allocation: the caller owns all
- * input, output and workspace buffers. Functions are stateless and reentrant. On failure they
- * return a negative mmseq_status and mmseq_last_error() describes it (thread-local).
+ * input, output and workspace buffers. Functions are stateless and reentrant: kernel selection
+ * and scratch space are per-call arguments; the only process-wide state is a write-once,
+ * per-device table of CU counts. Calls on different streams are independent as long as they do
+ * not share output or workspace buffers. On failure they return a negative mmseq_status and
+ * mmseq_last_error() describes it (thread-local).
  *
  * The reference has NO native layer: it is 100 % PyTorch, so each entry point
  * below replaces a group of PyTorch ops at the reference site cited next to it. The Python
@@ -64,7 +67,23 @@ const char* mmseq_version(void);
  *                        v = dropout(v) (optional, idx = (b*M + m)*N + n)
  *                        v += resid[m][n] (optional)   ;   if accumulate: v += C[m][n]
  *   A, B share in_dtype; C, resid, aux_out, dact_aux share out_dtype (aux ld = ldc).
+ *   variant: kernel selection for THIS call (tests and microbenchmarks cover every variant):
+ *     MMSEQ_GEMM_AUTO (default: 256 x 256 persistent NT/TN kernels for large problems,
+ *     128 x 128 double-buffer otherwise), MMSEQ_GEMM_DB128 (128 x 128 double-buffer only),
+ *     MMSEQ_GEMM_RING128 (128 x 128 four-slot ring only), MMSEQ_GEMM_BIG_ALWAYS (256 x 256
+ *     NT for every eligible NT problem), MMSEQ_GEMM_BIG_256x128 (256 x 128 NT, two blocks/CU),
+ *     MMSEQ_GEMM_GENERIC (register-staged kernel only).
+ *   workspace: caller-owned, 16-byte aligned device scratch for fp32 split-K partial slabs of
+ *     this call (NULL / 0 bytes = no split-K). Wgrad-shaped problems (few output tiles, long
+ *     K) split K across workgroups and reduce the slabs in a fixed order (bitwise reproducible).
+ *     It is only touched by work enqueued on `stream`, so concurrent calls on different
+ *     streams need different workspaces; mmseq_gemm_workspace_size() bounds what helps.
  * ------------------------------------------------------------------------------------------ */
+typedef enum {
+  MMSEQ_GEMM_GENERIC = 0, MMSEQ_GEMM_AUTO = 1, MMSEQ_GEMM_DB128 = 2, MMSEQ_GEMM_RING128 = 3,
+  MMSEQ_GEMM_BIG_ALWAYS = 4, MMSEQ_GEMM_BIG_256x128 = 5
+} mmseq_gemm_variant;
+
 mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch,
                         const void* A, int64_t lda, int64_t strideA,
                         const void* B, int64_t ldb, int64_t strideB,
@@ -72,25 +91,19 @@ mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch,
                         const float* bias, int act, void* aux_out, const void* dact_aux,
                         const void* resid, int64_t ldr, int64_t strideR,
                         float alpha, int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
-                        const mmseq_dropout* drop, mmseq_stream stream);
-
-/* Kernel selection (tests and microbenchmarks cover every variant): 1 = default (256 x 256 NT
- * kernel for large problems, 128 x 128 double-buffer otherwise), 2 = 128 x 128 double-buffer,
- * 3 = 128 x 128 ring only, 4 = 256 x 256 NT for every eligible NT problem, 0 = generic
- * register-staged kernel only. */
-void mmseq_gemm_set_fast(int enable);
-/* Registers a caller-owned device workspace for split-K partial slabs (fp32). With it, wgrad-shaped
- * TN GEMMs (few output tiles, long K, plain fp32 accumulate) split K across workgroups and reduce
- * the slabs in a fixed order (bitwise reproducible). The workspace must not be used concurrently
- * by GEMMs on different streams. NULL disables split-K. */
-void mmseq_gemm_set_workspace(void* ws, int64_t bytes);
+                        const mmseq_dropout* drop, int variant, void* workspace,
+                        int64_t workspace_bytes, mmseq_stream stream);
+/* Bytes of split-K workspace beyond which mmseq_gemm / mmseq_gemm_wgrad gain nothing for an
+ * M x N x K problem on the current device. */
+int64_t mmseq_gemm_workspace_size(int M, int N, int K);
 /* Weight + bias gradient of a Linear in one pass (replaces the wgrad GEMM and the bias column sum
  * of every nn.Linear backward on the path): C[M][N] += sum_k A[k][m] B[k][n] (A = dY [K][lda],
  * B = X [K][ldb], fp32 C) and, if bias_grad != NULL, bias_grad[m] += sum_k A[k][m] (fp32).
- * Deterministic (fixed-order split-K reductions). */
+ * Deterministic (fixed-order split-K reductions). variant / workspace as for mmseq_gemm. */
 mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int64_t lda, const void* B,
                               int64_t ldb, float* C, int64_t ldc, float* bias_grad,
-                              mmseq_dtype in_dtype, mmseq_stream stream);
+                              mmseq_dtype in_dtype, int variant, void* workspace,
+                              int64_t workspace_bytes, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused multi-head attention over a packed QKV activation (lxrt/modeling.py:398-425 with the
@@ -101,22 +114,21 @@ mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int64_t lda, c
  *   lse: [P][heads][T] f32 (log-sum-exp of the scaled, biased scores), written by fwd.
  * bwd: delta workspace [P][heads][T] f32; dqkv has the same packed layout as qkv (ld_dqkv).
  * drop: attention-probability dropout (lxrt:421), idx = ((p*heads + h)*T + q)*T + k.
+ * variant (per call, bf16 only): 1 = 128-row workgroups with LDS-DMA double-buffered K/V (or
+ * Q/dO) tiles and the delta = rowsum(dO * O) reduction fused into the dQ kernel; 0 = 64-row
+ * register-staged kernels (cross-check in the tests). fp32 always uses the latter.
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, void* out, int64_t ld_out, float* lse,
                             mmseq_dtype dtype, const mmseq_dropout* drop, uint64_t* keep_bits,
-                            mmseq_stream stream);
+                            int variant, mmseq_stream stream);
 mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, const void* out, int64_t ld_out, const void* dout,
                             int64_t ld_dout, const float* lse, float* delta, void* dqkv,
                             int64_t ld_dqkv, mmseq_dtype dtype, const mmseq_dropout* drop,
-                            const uint64_t* keep_bits, mmseq_stream stream);
-/* bf16 attention kernel selection: 1 (default) = 128-row workgroups with LDS-DMA double-buffered
- * K/V (or Q/dO) tiles and the delta = rowsum(dO * O) reduction fused into the dQ kernel;
- * 0 = 64-row register-staged kernels (cross-check in the tests). fp32 always uses the latter. */
-void mmseq_attn_set_fast(int enable);
+                            const uint64_t* keep_bits, int variant, mmseq_stream stream);
 /* Attention-probability dropout keep-mask cache (bf16 fast kernels): with keep_bits != NULL the
  * forward also stores its counter-based keep mask as bits (word [(p*heads + h)*T + q][kt] for key
  * tile kt < round_up_even(ceil(T/64)); key 64*kt + j at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 +

@@ -59,20 +59,21 @@ _SIGS = {
                                                        _vp, _c_i64, _c_i64, _vp, ctypes.c_int, _vp,
                                                        _vp, _vp, _c_i64, _c_i64, ctypes.c_float,
                                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                                       _dp, _vp]),
-    "mmseq_gemm_set_fast": (None, [ctypes.c_int]),
-    "mmseq_attn_set_fast": (None, [ctypes.c_int]),
+                                                       _dp, ctypes.c_int, _vp, _c_i64, _vp]),
+    "mmseq_gemm_workspace_size": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_gemm_wgrad": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _c_i64, _vp, _c_i64,
-                                                             _vp, ctypes.c_int, _vp]),
-    "mmseq_gemm_set_workspace": (None, [_vp, _c_i64]),
+                                                             _vp, ctypes.c_int, ctypes.c_int, _vp,
+                                                             _c_i64, _vp]),
     "mmseq_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
-                                                           ctypes.c_int, _dp, _vp, _vp]),
+                                                           ctypes.c_int, _dp, _vp, ctypes.c_int,
+                                                           _vp]),
     "mmseq_attn_keep_bits_words": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            _c_i64, _vp, _vp, _vp, _c_i64,
-                                                           ctypes.c_int, _dp, _vp, _vp]),
+                                                           ctypes.c_int, _dp, _vp, ctypes.c_int,
+                                                           _vp]),
     "mmseq_small_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 4 + [ctypes.c_float, _vp,
                                                                              _vp, _dp, _vp]),
     "mmseq_small_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float, _vp,
@@ -119,16 +120,28 @@ _SIGS = {
 EXPORTS = sorted(k for k in _SIGS)
 
 
+# Split-K slab workspaces, one per (device, stream): the C ABI takes the workspace per call and
+# only work enqueued on that stream touches it, so calls on different streams never share one.
+WORKSPACE_BYTES = 256 << 20
 _ws = {}
 
 
-def ensure_gemm_workspace(device, nbytes=256 << 20):
-    """Allocate (once per device) and register the split-K slab workspace."""
-    key = str(device)
-    if key not in _ws:
-        _ws[key] = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
-        lib().mmseq_gemm_set_workspace(_ws[key].data_ptr(), nbytes)
-    return _ws[key]
+def gemm_workspace(device, stream=None):
+    dev = torch.device(device)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), stream.cuda_stream)
+    buf = _ws.get(key)
+    if buf is None:
+        buf = _ws[key] = torch.empty(WORKSPACE_BYTES // 4, dtype=torch.float32, device=dev)
+    return buf
+
+
+# Per-call kernel selection (include/mmseq.h mmseq_gemm_variant / attention variant). The
+# defaults below are what the product path uses; tests and microbenchmarks switch them with
+# gemm_set_fast / attn_set_fast (Python-side defaults only: the C ABI holds no selection state).
+GEMM_AUTO = 1
+_sel = {"gemm": GEMM_AUTO, "attn": 1}
 
 
 def lib():
@@ -179,8 +192,7 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
          bias=None, act=0, aux=None, dact=None, resid=None, ldr=None, sR=0, alpha=1.0,
          accumulate=False, drop=None):
     _dev(A, B, C)
-    if not _ws:
-        ensure_gemm_workspace(A.device)
+    ws = gemm_workspace(A.device)
     if lda is None:
         lda = M if trans else K
     if ldb is None:
@@ -191,28 +203,31 @@ def gemm(A, B, C, M, N, K, *, trans=0, lda=None, ldb=None, ldc=None, batch=1, sA
         ldr = ldc
     _check(lib().mmseq_gemm(trans, M, N, K, batch, _p(A), lda, sA, _p(B), ldb, sB, _p(C), ldc, sC,
                             _p(bias), act, _p(aux), _p(dact), _p(resid), ldr, sR, alpha,
-                            int(accumulate), dt(A), dt(C), _d(drop), _stream()), "mmseq_gemm")
+                            int(accumulate), dt(A), dt(C), _d(drop), _sel["gemm"], ws.data_ptr(),
+                            ws.numel() * 4, _stream()), "mmseq_gemm")
 
 
 def gemm_wgrad(dy, x, gW, gb=None):
     """gW[out][in] += dy^T x and gb[out] += column sums of dy (fp32), dy [R][out], x [R][in]."""
     _dev(dy, x, gW)
-    if not _ws:
-        ensure_gemm_workspace(dy.device)
+    ws = gemm_workspace(dy.device)
     M, Nn = gW.shape
     R = dy.numel() // dy.shape[-1]
     _check(lib().mmseq_gemm_wgrad(M, Nn, R, _p(dy), dy.shape[-1], _p(x), x.shape[-1], _p(gW), Nn,
-                                  _p(gb), dt(dy), _stream()), "mmseq_gemm_wgrad")
+                                  _p(gb), dt(dy), _sel["gemm"], ws.data_ptr(), ws.numel() * 4,
+                                  _stream()), "mmseq_gemm_wgrad")
 
 
-def gemm_set_fast(enable):
-    lib().mmseq_gemm_set_fast(int(enable))
+def gemm_set_fast(variant):
+    """Default GEMM variant passed by this binding (mmseq_gemm_variant): 1 = auto (product),
+    2 = 128^2 double-buffer, 3 = 128^2 ring, 4 = 256^2 NT always, 5 = 256x128 NT, 0 = generic."""
+    _sel["gemm"] = int(variant)
 
 
 def attn_set_fast(enable):
-    """bf16 attention kernel selection: 1 = 128-row LDS-DMA pipelined kernels (default), 0 = the
-    64-row kernels (kept as a cross-check in the tests)."""
-    lib().mmseq_attn_set_fast(int(enable))
+    """bf16 attention variant passed by this binding: 1 = 128-row LDS-DMA pipelined kernels
+    (product), 0 = the 64-row kernels (kept as a cross-check in the tests)."""
+    _sel["attn"] = int(enable != 0)
 
 
 def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse,
@@ -220,7 +235,7 @@ def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out
     _dev(qkv, out, lse)
     _check(lib().mmseq_attn_fwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
                                 scale, _p(out), ld_out, _p(lse), dt(qkv), _d(drop), _p(keep_bits),
-                                _stream()), "mmseq_attn_fwd")
+                                _sel["attn"], _stream()), "mmseq_attn_fwd")
 
 
 def attn_keep_bits(P, T, heads, device):
@@ -233,7 +248,8 @@ def attn_bwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out
              ld_dout, lse, delta, dqkv, ld_dqkv, drop=None, keep_bits=None):
     _check(lib().mmseq_attn_bwd(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off, _p(key_bias),
                                 scale, _p(out), ld_out, _p(dout), ld_dout, _p(lse), _p(delta),
-                                _p(dqkv), ld_dqkv, dt(qkv), _d(drop), _p(keep_bits), _stream()),
+                                _p(dqkv), ld_dqkv, dt(qkv), _d(drop), _p(keep_bits), _sel["attn"],
+                                _stream()),
            "mmseq_attn_bwd")
 
 

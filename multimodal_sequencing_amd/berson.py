@@ -88,8 +88,18 @@ class BertForOrdering(nn.Module):
         self.hidden_dropout_prob = getattr(config, "hidden_dropout_prob", 0.1)  # :677
         self.para_dropout = getattr(args, "para_dropout", 0.1)  # train.py:2014, :881
         self._drops = K.EVAL
+        from .lxrt import _mark_stale
+        self.register_load_state_dict_post_hook(_mark_stale)
 
     # ------------------------------------------------------------------------------------
+    def ddp_units(self):
+        """(units, begin_stores) for trainer.GradAllReduce: the inner model's per-layer spans;
+        the head store completes as a whole before the inner model's backward begins."""
+        units = {}
+        if self.bert is not None:
+            units[id(self.bert.store)] = self.bert.grad_units()
+        return units, [self.store]
+
     def stores(self):
         return [self.bert.store, self.store] if self.bert is not None else [self.store]
 
@@ -276,6 +286,7 @@ class BertForOrdering(nn.Module):
         pnll = -lc.gather(-1, pairwise_labels.reshape(-1, 1)).view(B, npair)
         pmask = (torch.arange(npair, device=dev)[None] < pairs_num[:, None]).float()
         l_pair = ((pnll * pmask).sum(-1) / (pairs_num.float() + 1e-20)).sum() / B  # :1145-1172
+        self.last_loss_terms = (l_ptr.detach(), l_pair.detach())  # (pointer, pairwise) losses
         return (l_ptr + l_pair * self.pairwise_loss_lam,)
 
     # ------------------------------------------------------------------------------------

@@ -21,7 +21,6 @@ namespace {
 constexpr int HD = 64;       // head dim
 constexpr int QT = 64;       // rows per workgroup tile
 constexpr float NEG = -1e30f;
-int g_attn_fast = 1;  // bf16: 1 = 128-row DMA-pipelined kernels, 0 = 64-row kernels (tests)
 
 template <typename TI> struct ACfg;
 template <> struct ACfg<unsigned short> { static constexpr int LD = 80, VE = 8; };
@@ -1193,7 +1192,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
                                        const float* key_bias, float scale, void* out,
                                        int64_t ld_out, float* lse, mmseq_dtype dtype,
                                        const mmseq_dropout* drop, uint64_t* keep_bits,
-                                       mmseq_stream stream) {
+                                       int variant, mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   MMSEQ_REQUIRE(out && lse && ld_out >= heads * 64, "attn_fwd: bad out/lse");
@@ -1205,7 +1204,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   a.drop = make_drop(drop);
   dim3 grid((T + QT - 1) / QT, heads, P);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (dtype == MMSEQ_BF16 && g_attn_fast) {
+  if (dtype == MMSEQ_BF16 && variant) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;
@@ -1231,7 +1230,7 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
                                        const float* lse, float* delta, void* dqkv,
                                        int64_t ld_dqkv, mmseq_dtype dtype,
                                        const mmseq_dropout* drop, const uint64_t* keep_bits,
-                                       mmseq_stream stream) {
+                                       int variant, mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   const int ve = dtype == MMSEQ_BF16 ? 8 : 4;
@@ -1249,7 +1248,7 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   const int64_t rows = (int64_t)P * T;
   dim3 gd((unsigned)((rows + 3) / 4));
   dim3 grid((T + QT - 1) / QT, heads, P);
-  if (dtype == MMSEQ_BF16 && g_attn_fast) {
+  if (dtype == MMSEQ_BF16 && variant) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0 && aligned16(dqkv) && ld_dqkv % 8 == 0,
                   "attn_bwd: out / dqkv must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
@@ -1277,8 +1276,6 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   }
   return mmseq_check_launch("attn_bwd");
 }
-
-extern "C" void mmseq_attn_set_fast(int enable) { g_attn_fast = enable != 0; }
 
 extern "C" int64_t mmseq_attn_keep_bits_words(int P, int T, int heads) {
   const int64_t nkt2 = (((T + 63) / 64) + 1) & ~1;

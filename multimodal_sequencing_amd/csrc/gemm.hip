@@ -18,14 +18,48 @@
 #include <cstdlib>
 #include "gemm_common.h"
 
-static int g_disable_fast = 0;  // test hook: force the generic kernel
-// caller-provided split-K slab workspace (mmseq_gemm_set_workspace); stream-ordered use only
-static float* g_slab = nullptr;
-static int g_ring = 0;  // 1: BK=32 four-slot ring kernel, 0: BK=64 double-buffer kernel
-static int g_big = 1;   // 256 x 256 NT kernel: 1 for large problems, 2 always (tests)
-static int64_t g_slab_bytes = 0;
-static int g_nt_variant = 0;  // large NT: 0 = 256x256 one block/CU, 1 = 256x128 two blocks/CU
-static int g_num_cu = 256;  // persistent grid size (set from the device at first use)
+#include <atomic>
+
+// The ABI is stateless: kernel selection and the split-K slab workspace are per-call arguments.
+// The only process-wide state is this lazily filled, per-device, write-once CU-count table.
+static std::atomic<int> g_cu_table[64];
+
+static int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = g_cu_table[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  // MMSEQ_GEMM_CUS: persistent-grid size override for measurement (tools/gemm_epi_bench.py),
+  // read once per device
+  if (const char* e = getenv("MMSEQ_GEMM_CUS")) {
+    const int v = atoi(e);
+    if (v > 0 && v <= n) n = v;
+  }
+  g_cu_table[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+// Per-call kernel selection (mmseq_gemm `variant`, include/mmseq.h)
+struct GemmSel {
+  bool disable_fast;  // generic register-staged kernel only
+  int big;            // 256 x 256 NT / TN kernels: 1 for large problems, 2 always, 0 never
+  bool ring;          // BK=32 four-slot ring kernel instead of the BK=64 double-buffer kernel
+  int nt_variant;     // large NT: 0 = 256x256 one block/CU, 1 = 256x128 two blocks/CU
+  int num_cu;
+};
+
+static bool make_sel(int variant, GemmSel* s) {
+  if (variant < 0 || variant > 5) return false;
+  s->disable_fast = variant == 0;
+  s->big = variant == 1 ? 1 : ((variant == 4 || variant == 5) ? 2 : 0);
+  s->nt_variant = variant == 5 ? 1 : 0;
+  s->ring = variant == 3;
+  s->num_cu = device_cus();
+  return true;
+}
 
 namespace {
 using namespace mmseq_gemm_detail;
@@ -635,15 +669,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 }
 
 template <typename TO>
-hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s) {
-  if (!trans && g_big && a.splitk == 1 && batch == 1 && a.K % 128 == 0 &&
-      (g_big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256)) {
+hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s, const GemmSel& sel) {
+  if (!trans && sel.big && a.splitk == 1 && batch == 1 && a.K % 128 == 0 &&
+      (sel.big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256)) {
     hipError_t e;
-    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, g_num_cu, s, &e, g_nt_variant)) return e;
+    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, sel.num_cu, s, &e, sel.nt_variant)) return e;
   }
   const int tiles_m = (a.M + 127) / 128, tiles_n = (a.N + 127) / 128;
   dim3 grid(tiles_m * tiles_n, a.splitk > 1 ? a.splitk : batch);
-  if (g_ring) {
+  if (sel.ring) {
     if (trans)
       hipLaunchKernelGGL((gemm_ring_kernel<TO, true>), grid, dim3(256), 0, s, a, tiles_n);
     else
@@ -661,27 +695,14 @@ inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 }  // namespace
 
-extern "C" void mmseq_gemm_set_fast(int enable) {
-  // 1 = default (256^2 NT for large problems, double-buffer 128^2 otherwise), 2 = double-buffer
-  // 128^2 only, 3 = ring 128^2 only, 4 = 256^2 NT whenever its preconditions hold, 0 = generic
-  g_disable_fast = enable == 0;
-  g_big = enable == 1 ? 1 : ((enable == 4 || enable == 5) ? 2 : 0);
-  g_nt_variant = enable == 5 ? 1 : 0;
-  g_ring = enable == 3;
-}
-
-extern "C" void mmseq_gemm_set_workspace(void* ws, int64_t bytes) {
-  g_slab = reinterpret_cast<float*>(ws);
-  g_slab_bytes = ws ? bytes : 0;
-}
-
 extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, const void* A,
                                    int64_t lda, int64_t strideA, const void* B, int64_t ldb,
                                    int64_t strideB, void* C, int64_t ldc, int64_t strideC,
                                    const float* bias, int act, void* aux_out, const void* dact_aux,
                                    const void* resid, int64_t ldr, int64_t strideR, float alpha,
                                    int accumulate, mmseq_dtype in_dtype, mmseq_dtype out_dtype,
-                                   const mmseq_dropout* drop, mmseq_stream stream) {
+                                   const mmseq_dropout* drop, int variant, void* workspace,
+                                   int64_t workspace_bytes, mmseq_stream stream) {
   MMSEQ_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes M=%d N=%d K=%d b=%d",
                 M, N, K, batch);
   MMSEQ_REQUIRE(A && B && C, "gemm: null operand");
@@ -694,20 +715,15 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   } else {
     MMSEQ_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gemm TN: ld too small");
   }
+  MMSEQ_REQUIRE(workspace_bytes >= 0 && (workspace || workspace_bytes == 0) &&
+                    ((uintptr_t)workspace & 15) == 0,
+                "gemm: workspace must be 16-byte aligned (or NULL with 0 bytes)");
+  GemmSel sel;
+  MMSEQ_REQUIRE(make_sel(variant, &sel), "gemm: bad variant %d", variant);
   if (M == 0 || N == 0) return MMSEQ_OK;
-  static int cu_init = 0;
-  if (!cu_init) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      g_num_cu = n;
-    // MMSEQ_GEMM_CUS: persistent-grid size override for measurement (tools/gemm_epi_bench.py)
-    if (const char* e = getenv("MMSEQ_GEMM_CUS")) {
-      const int v = atoi(e);
-      if (v > 0 && v <= g_num_cu) g_num_cu = v;
-    }
-    cu_init = 1;
-  }
+  float* const g_slab = reinterpret_cast<float*>(workspace);
+  const int64_t g_slab_bytes = workspace ? workspace_bytes : 0;
+  const int g_num_cu = sel.num_cu;
   GemmArgs a;
   a.M = M; a.N = N; a.K = K;
   a.A = A; a.lda = lda; a.sA = strideA;
@@ -725,7 +741,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   a.vec_c = ((uintptr_t)C % (vc * esz) == 0) && ldc % vc == 0 && strideC % vc == 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
-  const bool fast_ok = in_dtype == MMSEQ_BF16 && a.vec_ok && !g_disable_fast &&
+  const bool fast_ok = in_dtype == MMSEQ_BF16 && a.vec_ok && !sel.disable_fast &&
                        (trans ? (M % 8 == 0 && N % 8 == 0) : (K % 64 == 0)) &&
                        (int64_t)M * N >= 128 * 128;
   a.splitk = 1; a.kchunk = K; a.slab = nullptr;
@@ -736,7 +752,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
                        !a.drop.thr &&
                        out_dtype == MMSEQ_F32 && batch == 1 && ldc % 4 == 0 && al16(C);
     // weight gradients: 256 x 256 TN kernel, K split so that (tiles x splits) fills the CUs
-    if (trans && plain && g_big) {
+    if (trans && plain && sel.big) {
       const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
       int S2 = t256 < g_num_cu ? g_num_cu / t256 : 1;
       if (S2 > K / 1024) S2 = K / 1024 > 0 ? K / 1024 : 1;
@@ -773,7 +789,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
       S = (K + a.kchunk - 1) / a.kchunk;
       a.splitk = S;
       a.slab = g_slab;
-      e = launch_fast<float>(trans, a, 1, s);
+      e = launch_fast<float>(trans, a, 1, s, sel);
       if (e == hipSuccess) {
         int64_t t4 = (int64_t)M * N / 4;
         unsigned blocks = (unsigned)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
@@ -782,8 +798,8 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
         e = hipGetLastError();
       }
     } else {
-      e = out_dtype == MMSEQ_BF16 ? launch_fast<unsigned short>(trans, a, batch, s)
-                                  : launch_fast<float>(trans, a, batch, s);
+      e = out_dtype == MMSEQ_BF16 ? launch_fast<unsigned short>(trans, a, batch, s, sel)
+                                  : launch_fast<float>(trans, a, batch, s, sel);
     }
   } else if (in_dtype == MMSEQ_F32 && out_dtype == MMSEQ_F32 && batch == 1 && g_slab &&
              ((M + 127) / 128) * ((N + 127) / 128) < 128 && K >= 256) {
@@ -827,21 +843,56 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   return MMSEQ_OK;
 }
 
+// Upper bound of the split-K slab bytes any path of mmseq_gemm / mmseq_gemm_wgrad picks for this
+// shape on the current device (less workspace only lowers the split count).
+extern "C" int64_t mmseq_gemm_workspace_size(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int64_t cus = device_cus(), MN = (int64_t)M * N;
+  int64_t best = 0;
+  const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  int64_t s2 = t256 < cus ? cus / t256 : 1;
+  if (s2 > K / 1024) s2 = K / 1024 > 0 ? K / 1024 : 1;
+  if (s2 > 1) best = s2 * (M + MN) * 4;
+  const int64_t tiles = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (tiles < 512) {
+    int64_t s = (1024 + tiles - 1) / tiles;
+    if (s > K / 1024) s = K / 1024;
+    if (s > 1 && s * MN * 4 > best) best = s * MN * 4;
+  }
+  if (tiles < 128 && K >= 256) {
+    int64_t s = (cus + tiles - 1) / tiles;
+    if (s > K / 128) s = K / 128;
+    if (s > 1 && s * MN * 4 > best) best = s * MN * 4;
+  }
+  return best;
+}
+
 // Weight gradient with the fused bias gradient (include/mmseq.h): C[M][N] += A^T B and
 // bias_grad[m] += sum_k A[k][m]. bf16 operands with an eligible shape take the 256 x 256 TN
 // kernel (column sums of the A fragments on the VALU beside the MFMAs); anything else runs
 // mmseq_gemm plus a separate column-sum kernel.
 extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int64_t lda,
                                          const void* B, int64_t ldb, float* C, int64_t ldc,
-                                         float* bias_grad, mmseq_dtype in_dtype,
+                                         float* bias_grad, mmseq_dtype in_dtype, int variant,
+                                         void* workspace, int64_t workspace_bytes,
                                          mmseq_stream stream) {
   MMSEQ_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_wgrad: bad sizes");
   MMSEQ_REQUIRE(A && B && C, "gemm_wgrad: null operand");
   MMSEQ_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gemm_wgrad: ld too small");
   MMSEQ_REQUIRE(in_dtype == MMSEQ_F32 || in_dtype == MMSEQ_BF16, "gemm_wgrad: bad dtype");
+  MMSEQ_REQUIRE(workspace_bytes >= 0 && (workspace || workspace_bytes == 0) &&
+                    ((uintptr_t)workspace & 15) == 0,
+                "gemm_wgrad: workspace must be 16-byte aligned (or NULL with 0 bytes)");
+  GemmSel sel;
+  MMSEQ_REQUIRE(make_sel(variant, &sel), "gemm_wgrad: bad variant %d", variant);
   if (M == 0 || N == 0 || K == 0) return MMSEQ_OK;
+  float* const g_slab = reinterpret_cast<float*>(workspace);
+  const int64_t g_slab_bytes = workspace ? workspace_bytes : 0;
+  const int g_num_cu = sel.num_cu;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (in_dtype == MMSEQ_BF16 && g_big && bias_grad) {
+  // the split-K reduction does f32x4 read-modify-writes on C: 16-byte aligned rows only
+  const bool c_vec = ((uintptr_t)C & 15) == 0 && ldc % 4 == 0;
+  if (in_dtype == MMSEQ_BF16 && sel.big && bias_grad && c_vec) {
     GemmArgs t = {};
     t.M = M; t.N = N; t.K = K;
     t.A = A; t.lda = lda; t.B = B; t.ldb = ldb; t.C = C; t.ldc = ldc;
@@ -874,7 +925,8 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
     }
   }
   mmseq_status st = mmseq_gemm(1, M, N, K, 1, A, lda, 0, B, ldb, 0, C, ldc, 0, nullptr, 0, nullptr,
-                               nullptr, nullptr, 0, 0, 1.0f, 1, in_dtype, MMSEQ_F32, nullptr, stream);
+                               nullptr, nullptr, 0, 0, 1.0f, 1, in_dtype, MMSEQ_F32, nullptr,
+                               variant, workspace, workspace_bytes, stream);
   if (st || !bias_grad) return st;
   if (in_dtype == MMSEQ_BF16)
     hipLaunchKernelGGL(colsum_simple_kernel<unsigned short>, dim3((M + 255) / 256), dim3(256), 0, s,

@@ -85,11 +85,22 @@ EVAL = Dropouts(0, False)
 
 
 class LayerRefs:
-    """Names of one layer's parameters inside a ParamStore (resolved once)."""
+    """Names of one layer's parameters inside a ParamStore (resolved once). `span` is the
+    contiguous grad-buffer range the layer's backward completes (reported to the data-parallel
+    reducer through ParamStore.grad_ready)."""
 
     def __init__(self, store, **names):
         self.store = store
         self.__dict__.update(names)
+        self.span = store.span(self.names())
+
+    def names(self):
+        out = []
+        for k, v in self.__dict__.items():
+            if k in ("store", "span"):
+                continue
+            out += v if isinstance(v, list) else [v]
+        return out
 
 
 # ================================================================================================
@@ -135,6 +146,7 @@ class BertLayerFn(torch.autograd.Function):
         x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2 = ctx.saved_tensors
         L, P, T, heads, (d_att, d_o, d_out) = ctx.meta
         st = L.store
+        st.grad_begin()
         H = x.shape[-1]
         dy = dy.contiguous()
         R = x.shape[0]
@@ -165,6 +177,7 @@ class BertLayerFn(torch.autograd.Function):
                    H, do, H, lse, delta, dqkv, 3 * H, drop=d_att, keep_bits=ctx.kbits)
         ctx.kbits = None
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
+        st.grad_ready(L.span)
         dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None
 
@@ -206,6 +219,7 @@ class VitBlockFn(torch.autograd.Function):
         h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact = ctx.saved_tensors
         L, P, T, heads = ctx.meta
         st = L.store
+        st.grad_begin()
         W = h.shape[-1]
         R = h.shape[0]
         dx2 = dx2.contiguous()
@@ -228,6 +242,7 @@ class VitBlockFn(torch.autograd.Function):
         dh = torch.empty_like(h)
         N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
                         dx1, _rows(W), st.g(L.ln1_w), st.g(L.ln1_b))
+        st.grad_ready(L.span)
         return dh, None, None, None, None, None, None
 
 
@@ -273,6 +288,7 @@ class VitStemFn(torch.autograd.Function):
         patches = torch.empty(P * 2 * gg, 3 * patch * patch, device=x0.device, dtype=cdtype)
         N.vit_im2col(B, Nst, pairs.shape[1], R_, patch, images, pairs, patches)  # recompute
         _wgrad(dpo, patches, st.g(L.conv_w).view(W, -1))
+        st.grad_ready(L.span)
         return None, None, None, None, None, None, None
 
 
@@ -299,6 +315,7 @@ class VitProjFn(torch.autograd.Function):
         N.gemm(h, dv, gp, gp.shape[0], gp.shape[1], R, trans=1, lda=h.shape[-1], ldb=dv.shape[-1],
                accumulate=True)
         dh = _dgrad(dv, st.w(L.proj))  # dh[r][w] = sum_e dv[r][e] proj[w][e]
+        st.grad_ready(L.span)
         return dh, None, None
 
 
@@ -354,6 +371,8 @@ class JointInputFn(torch.autograd.Function):
                             st.f32(L.vln_w), dvpre, _rows(H), None, _rows(H), st.g(L.vln_w),
                             st.g(L.vln_b), drop_dy=drops[1])
             _wgrad(dvpre, vout, st.g(L.v_w), st.g(L.v_b))
+        st.grad_ready(L.span)
+        if has_v:
             dvout = _dgrad(dvpre, st.wt(L.v_w))
         return dvout, None, None, None, None, None, None, None, None, None, None, None
 

@@ -101,8 +101,15 @@ def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25):
                Spec("encoder.visual_pos.y_position_embedding.weight", (pos_num, E), normal(std)),
                Spec("encoder.visual_token_type.token_type_embedding.weight",
                     (5, E), normal(std))]  # hard-coded max_story_length = 5 (lxrt:666-667)
-    sp += linear_specs("pooler.dense", H, H, std=std, transpose=False)
+    sp += linear_specs("pooler.dense", H, H, std=std)
     return sp
+
+
+def _mark_stale(module, incompatible_keys):
+    """load_state_dict post-hook: the parameters are views of the master buffer, so a load
+    rewrites master weights behind the compute-dtype / transposed shadows."""
+    for s in module.stores() if hasattr(module, "stores") else [module.store]:
+        s.shadow_stale = True
 
 
 class LXRTModel(nn.Module):
@@ -129,6 +136,7 @@ class LXRTModel(nn.Module):
         attach_tree(self, self.store.params)
         self._anchor = torch.zeros((), device=device, requires_grad=True)
         self._build_refs()
+        self.register_load_state_dict_post_hook(_mark_stale)
         self.dropout_seed = kw.get("seed", 0)  # fold the rank in for data parallel (trainer.py)
         self._n_fwd = 0
 
@@ -162,9 +170,11 @@ class LXRTModel(nn.Module):
             eln_b=e + "LayerNorm.bias", v_w=v + "visn_fc.weight", v_b=v + "visn_fc.bias",
             vln_w=v + "visn_layer_norm.weight", vln_b=v + "visn_layer_norm.bias")
         if not self.text_part:
+            # the projection lies between the positional embedding and conv1 in the buffer, so the
+            # stem's grad span includes it (VitProjFn's backward runs before the stem's)
             self.stem_refs = K.LayerRefs(st, conv_w=VIT + "conv1.weight", cls=VIT + "class_embedding",
                                          pos=VIT + "positional_embedding", ln_w=VIT + "ln_pre.weight",
-                                         ln_b=VIT + "ln_pre.bias")
+                                         ln_b=VIT + "ln_pre.bias", proj_in_span=VIT + "proj")
             self.proj_refs = K.LayerRefs(st, proj=VIT + "proj")
             self.block_refs = []
             for i in range(self.vision["layers"]):
@@ -175,6 +185,16 @@ class LXRTModel(nn.Module):
                     ln1_w=b + "ln_1.weight", ln1_b=b + "ln_1.bias", fc_w=b + "mlp.c_fc.weight",
                     fc_b=b + "mlp.c_fc.bias", proj_w=b + "mlp.c_proj.weight",
                     proj_b=b + "mlp.c_proj.bias", ln2_w=b + "ln_2.weight", ln2_b=b + "ln_2.bias"))
+
+    def grad_units(self):
+        """Contiguous grad-buffer spans completed by one layer-level backward each (for the
+        overlapped data-parallel all-reduce, trainer.GradAllReduce). The ViT projection sits
+        inside the stem's span in the buffer, so it is reported with the stem."""
+        units = [L.span for L in self.layer_refs] + [self.input_refs.span]
+        if not self.text_part:
+            units += [L.span for L in self.block_refs]
+            units.append(self.stem_refs.span)
+        return [u for u in units if u is not None]
 
     @property
     def compute_dtype(self):
@@ -247,5 +267,7 @@ class LXRTModel(nn.Module):
                                       pairs_list)
         lang = joint[:, :Lt]
         visn = joint[:, Lt:] if joint.shape[1] > Lt else None
-        # the pooler is computed but unused on the BERSON path (:1586); expose lang[:,0] as pooled
-        return (lang, visn), lang[:, 0]
+        # BertPooler (:1125-1137, tanh commented out in the reference): dense(lang[:, 0]) (:1584)
+        pooled = K.LinearFn.apply(lang[:, 0], self._anchor, self.store, "pooler.dense.weight",
+                                  "pooler.dense.bias", 0)
+        return (lang, visn), pooled

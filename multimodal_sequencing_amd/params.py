@@ -89,6 +89,33 @@ class ParamStore:
             p.grad = self.grad[o:o + _numel(s.shape)].view(s.shape)
             self.params[s.name] = p
         self.shadow_stale = True
+        # data-parallel hooks (trainer.GradAllReduce): a layer-level autograd Function reports
+        # its grad span at the end of its backward (grad_ready) and its start (grad_begin)
+        self.grad_hook = None
+        self.begin_hook = None
+
+    def span(self, names):
+        """[lo, hi) of the buffer holding `names` (present ones), hi rounded up to the alignment
+        so the dead padding after a unit belongs to it."""
+        lo, hi = None, None
+        for n in names:
+            if n not in self.offsets:
+                continue
+            o = self.offsets[n]
+            e = o + _numel(self._spec(n).shape)
+            lo = o if lo is None else min(lo, o)
+            hi = e if hi is None else max(hi, e)
+        if lo is None:
+            return None
+        return (lo, min(self.numel, (hi + ALIGN - 1) // ALIGN * ALIGN))
+
+    def grad_ready(self, span):
+        if self.grad_hook is not None and span is not None:
+            self.grad_hook(self, span)
+
+    def grad_begin(self):
+        if self.begin_hook is not None:
+            self.begin_hook(self)
 
     def _alloc_shadows(self):
         if self.compute_dtype == torch.float32:

@@ -17,13 +17,37 @@ from . import _native as N
 
 
 def linear_warmup_lr(step, base_lr, warmup, total):
-    """transformers get_linear_schedule_with_warmup (train.py:186-190)."""
+    """transformers get_linear_schedule_with_warmup lambda (train.py:186-190) at scheduler step
+    `step` (0-based: LambdaLR evaluates lambda(0) at construction)."""
     if step < warmup:
         return base_lr * step / max(1, warmup)
     return base_lr * max(0.0, (total - step) / max(1, total - warmup))
 
 
+def distributed_indices(n, world, rank, shuffle=True, seed=0, epoch=0):
+    """torch.utils.data.DistributedSampler's index rule (train.py:158-161: the sampler is built
+    with its defaults and never gets set_epoch, so epoch stays 0): a seeded permutation (or
+    arange), padded by wrapping to a multiple of `world`, then every world-th index from `rank`."""
+    if shuffle:
+        g = torch.Generator()
+        g.manual_seed(seed + epoch)
+        idx = torch.randperm(n, generator=g).tolist()
+    else:
+        idx = list(range(n))
+    per = math.ceil(n / world)
+    total = per * world
+    pad = total - len(idx)
+    if pad > 0:
+        idx += (idx * math.ceil(pad / len(idx)))[:pad]
+    return idx[rank:total:world]
+
+
 class FusedAdamW:
+    """transformers-3.4 AdamW + get_linear_schedule_with_warmup + clip_grad_norm_, one fused
+    kernel per flat store. The k-th update (1-based) uses lr = lambda(k - 1), because the
+    reference builds LambdaLR (lambda(0) at construction) and calls scheduler.step() after
+    optimizer.step() (train.py:185-190, 361-362); Adam's bias correction uses k."""
+
     def __init__(self, stores, lr=5e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  max_grad_norm=1.0, warmup=100, total_steps=10 ** 9):
         self.stores = stores
@@ -36,9 +60,13 @@ class FusedAdamW:
         dev = stores[0].master.device
         self._ss = torch.zeros(len(stores) + 1, device=dev)
 
+    def current_lr(self):
+        """lr the next step() applies (scheduler.get_last_lr() before that step)."""
+        return linear_warmup_lr(self.step_count, self.lr, self.warmup, self.total)
+
     def step(self):
+        lr = self.current_lr()
         self.step_count += 1
-        lr = linear_warmup_lr(self.step_count, self.lr, self.warmup, self.total)
         # global grad norm over all stores (clip_grad_norm_ over model.parameters())
         for i, s in enumerate(self.stores):
             N.sumsq(s.grad, self._ss[i:i + 1])
@@ -61,28 +89,140 @@ class FusedAdamW:
 
 
 class GradAllReduce:
-    """Bucketed mean all-reduce of the flat grad buffers over RCCL (backend "nccl" on ROCm)."""
+    """Data-parallel gradient mean over RCCL (backend "nccl" on ROCm), overlapped with backward.
 
-    def __init__(self, stores, bucket_mb=64):
-        self.stores = stores
-        self.bucket = max(1, int(bucket_mb * (1 << 20)) // 4)
+    The reference wraps the model in DDP (train.py:217-221), whose reducer all-reduces 25 MB
+    buckets from autograd hooks. Here every store's flat grad buffer is cut into contiguous
+    buckets (<= bucket_mb) at the boundaries of its backward units — one unit per layer-level
+    autograd Function (a BERT layer, a ViT block, the stem, the projection, the joint input),
+    each a contiguous span of the buffer. The Functions report their unit at the end of their
+    backward (ParamStore.grad_ready); a bucket's async all-reduce is issued as soon as every unit
+    overlapping it has reported, so RCCL runs on its own stream beside the remaining backward.
+    Spans no unit covers (parameters without a gradient on this path, or written by ops that
+    do not report) form their own buckets, issued by finish(). Stores listed in `begin_units`
+    count as complete when the first unit of another store reports a backward begin (the BERSON
+    head: autograd runs all of its nodes before the inner model's last layer). Only the last
+    micro-batch's backward is armed; finish() issues what is left and waits for every bucket.
+    """
 
-    def __call__(self):
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-            return
-        world = dist.get_world_size()
-        avg = dist.get_backend() == "nccl"  # RCCL has ReduceOp.AVG; gloo (CPU tests) does not
-        works = []
+    def __init__(self, stores, bucket_mb=64, units=None, begin_units=(), group=None):
+        self.stores = list(stores)
+        self.cap = max(1, int(bucket_mb * (1 << 20)) // 4)
+        self.group = group
+        self.armed = False
+        self.works = []
+        self.begin_units = set(id(s) for s in begin_units)
+        units = units or {}
+        self.plan = {}
         for s in self.stores:
-            g = s.grad
-            for o in range(0, g.numel(), self.bucket):
-                op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
-                works.append((dist.all_reduce(g[o:o + self.bucket], op=op, async_op=True),
-                              g[o:o + self.bucket]))
-        for w, chunk in works:
+            spans = list(units.get(id(s), []))
+            if id(s) in self.begin_units:
+                spans = [(0, s.numel)]
+            self.plan[id(s)] = self._make_buckets(s, spans)
+            s.grad_hook = self._ready
+            s.begin_hook = self._begin
+
+    @staticmethod
+    def _pieces(numel, spans):
+        """Partition [0, numel) into (lo, hi, unit index or -1) pieces in memory order."""
+        cover = sorted((lo, hi, u) for u, (lo, hi) in enumerate(spans))
+        out, pos = [], 0
+        for lo, hi, u in cover:
+            if lo < pos:
+                raise ValueError("grad units overlap")
+            if lo > pos:
+                out.append((pos, lo, -1))
+            out.append((lo, hi, u))
+            pos = hi
+        if pos < numel:
+            out.append((pos, numel, -1))
+        return out
+
+    def _make_buckets(self, store, spans):
+        """Buckets = contiguous [lo, hi) ranges: runs of whole units up to the cap (a unit larger
+        than the cap is one bucket), and cap-sized pieces of the uncovered ranges."""
+        buckets, cur = [], None  # bucket = [lo, hi, unit set, orphan]
+        for lo, hi, u in self._pieces(store.numel, spans):
+            if u < 0:
+                while lo < hi:
+                    take = min(hi - lo, self.cap)
+                    buckets.append([lo, lo + take, set(), True])
+                    lo += take
+                cur = None
+                continue
+            if cur is None or cur[1] - cur[0] + (hi - lo) > self.cap:
+                cur = [lo, lo, set(), False]
+                buckets.append(cur)
+            cur[1] = hi
+            cur[2].add(u)
+        span2unit = {tuple(sp): i for i, sp in enumerate(spans)}
+        unit2b = {u: [j for j, bk in enumerate(buckets) if u in bk[2]] for u in range(len(spans))}
+        return {"buckets": buckets, "span2unit": span2unit, "unit2b": unit2b}
+
+    def _world(self):
+        if not (dist.is_available() and dist.is_initialized()):
+            return 1
+        return dist.get_world_size(self.group)
+
+    def arm(self, on):
+        """Arm (last micro-batch) or disarm the backward-driven all-reduce."""
+        self.armed = bool(on) and self._world() > 1
+        if self.armed:
+            self.works = []
+            for s in self.stores:
+                pl = self.plan[id(s)]
+                pl["pending"] = [set(b[2]) for b in pl["buckets"]]
+                pl["fired"] = [False] * len(pl["buckets"])
+
+    def _fire(self, store, j):
+        pl = self.plan[id(store)]
+        if pl["fired"][j]:
+            return
+        pl["fired"][j] = True
+        lo, hi = pl["buckets"][j][:2]
+        chunk = store.grad[lo:hi]
+        avg = dist.get_backend(self.group) == "nccl"  # RCCL has ReduceOp.AVG; gloo does not
+        op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
+        self.works.append((dist.all_reduce(chunk, op=op, group=self.group, async_op=True),
+                           chunk, avg))
+
+    def _ready(self, store, span):
+        if not self.armed:
+            return
+        pl = self.plan[id(store)]
+        u = pl["span2unit"].get(tuple(span))
+        if u is None:
+            return
+        for j in pl["unit2b"][u]:
+            pl["pending"][j].discard(u)
+            if not pl["pending"][j] and not pl["buckets"][j][3]:
+                self._fire(store, j)
+
+    def _begin(self, store):
+        if not self.armed:
+            return
+        for s in self.stores:
+            if id(s) in self.begin_units and s is not store:
+                self._ready(s, (0, s.numel))
+
+    def finish(self):
+        """Issue every bucket not yet issued and wait for all (grads are the mean afterwards)."""
+        world = self._world()
+        if world == 1:
+            return
+        if not self.armed:
+            self.arm(True)
+        for s in self.stores:
+            for j in range(len(self.plan[id(s)]["buckets"])):
+                self._fire(s, j)
+        for w, chunk, avg in self.works:
             w.wait()
             if not avg:
                 chunk.div_(world)
+        self.works = []
+        self.armed = False
+
+    __call__ = finish
 
 
 def train_step(model, optimizer, batches, reducer=None):
@@ -90,12 +230,14 @@ def train_step(model, optimizer, batches, reducer=None):
     Returns the (device) mean loss."""
     total = sum(b["input_ids"].shape[0] for b in batches)
     loss_sum = None
-    for b in batches:
+    for i, b in enumerate(batches):
+        if reducer is not None:
+            reducer.arm(i == len(batches) - 1)
         loss = model(b)[0] * (b["input_ids"].shape[0] / total)
         loss.backward()
         loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
     if reducer is not None:
-        reducer()
+        reducer.finish()
     optimizer.step()
     model.zero_grad()
     return loss_sum

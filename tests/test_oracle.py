@@ -54,3 +54,18 @@ def test_beam_order_matches_reference(name):
             pair = O.prepare_berson_inputs(d["input_ids"][b:b + 1], d["labels"][b:b + 1], cfg["N"])
             enc = O.encode(params, pair, images[b:b + 1], cfg)
             assert O.beam_order(params, enc) == list(d["order"][b])
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_product_pair_expansion_bit_exact(name):
+    """The product's vectorised pair expansion (multimodal_sequencing_amd/process_inputs.py)
+    reproduces the reference's prepare_berson_inputs tensors bit for bit (pair:: fixtures)."""
+    from multimodal_sequencing_amd.process_inputs import prepare_berson_inputs
+    meta, d, _ = load_fixture(name)
+    out = prepare_berson_inputs(d["input_ids"], d["labels"], meta["config"]["N"])
+    for k in ["input_ids", "attention_mask", "token_type_ids", "pairs_list", "passage_length",
+              "pairs_num", "sep_positions", "ground_truth", "mask_cls", "pairwise_labels"]:
+        ref = d["pair::" + k]
+        got = out[k].numpy()
+        assert got.dtype == np.int64 and got.shape == ref.shape, (k, got.shape, ref.shape)
+        assert np.array_equal(got, ref), k

@@ -131,3 +131,42 @@ def test_train_mode_dropout_gradient_is_consistent():
         vals.append(loss_at(0).item())
     fd = (vals[0] - vals[1]) / (2 * eps)
     assert abs(fd - gn) < 2e-2 * gn, (fd, gn)
+
+
+def _order_nll(m, inp, order):
+    """Total pointer NLL of `order` for one story = its beam-search score (sum over steps of
+    -log p, the last step forced): the teacher-forced pointer loss times (N - 1)."""
+    with torch.no_grad():
+        m({**inp, "labels": torch.tensor([order])})
+    N = len(order)
+    return float(m.last_loss_terms[0]) * (N - 1)
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_bf16_beam_order_matches_reference(name):
+    """bf16 perf mode (the benchmarked dtype) yields the reference's ordering on every fixture
+    story, except at a reported near-tie: when the orders differ, the fp32 model
+    must score both within NEAR_TIE of each other (near-ties are reported, not
+    silently accepted — the message and the printed line carry the margin)."""
+    NEAR_TIE = 5e-3  # total NLL over the story (~8 nats here); measured gaps 1e-4 - 4e-4
+    meta, d, params = load_fixture(name)
+    m = model_zoo.build_from_golden(meta["config"], device="cuda", dtype=torch.bfloat16)
+    m.load_state_dict(params)
+    m.eval()
+    m32 = None
+    for b in range(d["input_ids"].shape[0]):
+        inp = {"input_ids": torch.from_numpy(d["input_ids"][b:b + 1]),
+               "labels": torch.from_numpy(d["labels"][b:b + 1]),
+               "images": torch.from_numpy(d["images"][b:b + 1]).cuda()}
+        order = berson_pointer_network(m.args, m, None, inp)
+        ref = [int(x) for x in d["order"][b]]
+        if order == ref:
+            continue
+        if m32 is None:
+            m32 = model_zoo.build_from_golden(meta["config"], device="cuda", dtype=torch.float32)
+            m32.load_state_dict(params)
+            m32.eval()
+        gap = _order_nll(m32, inp, order) - _order_nll(m32, inp, ref)
+        print(f"NEAR-TIE {name} story {b}: bf16 order {order} vs reference {ref}, fp32 score gap "
+              f"{gap:.3e}")
+        assert abs(gap) < NEAR_TIE, (name, b, order, ref, gap)
