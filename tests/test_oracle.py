@@ -69,3 +69,31 @@ def test_product_pair_expansion_bit_exact(name):
         got = out[k].numpy()
         assert got.dtype == np.int64 and got.shape == ref.shape, (k, got.shape, ref.shape)
         assert np.array_equal(got, ref), k
+
+
+def test_oracle_real_config3_story():
+    """The oracle (also the bench's cpu_baseline) reproduces the reference at the benchmark's
+    real shape: one config-3 story (ViT-B/16 + 12 x 768, T = 513), loss and gradient norms."""
+    import json
+    import os
+    from counter_init import counter_state_dict
+    from golden_util import GOLDEN
+    from make_golden_real import real_inputs
+    from multimodal_sequencing_amd import model_zoo
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    meta = json.load(open(os.path.join(GOLDEN, "real_config3.json")))
+    d = dict(np.load(os.path.join(GOLDEN, "real_config3.npz")))
+    shapes = {k: tuple(v.shape) for k, v in
+              model_zoo.build_preset("config3", device="cpu", dtype=torch.float32).state_dict().items()}
+    params = {k: torch.from_numpy(v).requires_grad_(True) for k, v in counter_state_dict(shapes).items()}
+    ids, labels, images = real_inputs(meta["input_seed"])
+    cfg = {"N": 5, "heads": 12, "inter_heads": 8, "text_only": False, "vit_heads": None}
+    loss, _, _ = O.forward_loss(params, ids, labels, torch.from_numpy(images), cfg)
+    loss.backward()
+    assert abs(loss.item() - float(d["loss"])) < 1e-5, (loss.item(), float(d["loss"]))
+    gn = sum(float((p.grad.double() ** 2).sum()) for p in params.values() if p.grad is not None) ** 0.5
+    assert abs(gn - float(d["grad_norm"])) < 1e-5 * float(d["grad_norm"])
+    for k in d:
+        if k.startswith("gn::"):
+            g = params[k[4:]].grad
+            assert abs(float(g.double().norm()) - float(d[k])) <= 1e-4 * float(d[k]) + 1e-6, k
