@@ -224,10 +224,11 @@ def gemm_set_fast(variant):
     _sel["gemm"] = int(variant)
 
 
-def attn_set_fast(enable):
-    """bf16 attention variant passed by this binding: 1 = 128-row LDS-DMA pipelined kernels
-    (product), 0 = the 64-row kernels (kept as a cross-check in the tests)."""
-    _sel["attn"] = int(enable != 0)
+def attn_set_fast(variant):
+    """bf16 attention variant passed by this binding: 2 = 32x32x16-MFMA forward (product),
+    1 = 128-row 16x16x32 LDS-DMA pipelined kernels, 0 = the 64-row kernels (cross-checks in the
+    tests). The backward uses the 128-row kernels for any nonzero variant."""
+    _sel["attn"] = int(variant)
 
 
 def attn_fwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out, lse,

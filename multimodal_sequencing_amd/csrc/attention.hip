@@ -15,6 +15,7 @@
 //            dK^T += Q^T dS take P / dS straight from the accumulators.
 //      dq:   per query tile, sweep the keys with the swapped form; dQ^T += K^T dS^T.
 #include "gemm_common.h"
+#include <type_traits>
 
 namespace {
 
@@ -805,6 +806,305 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
   }
 }
 
+// ---- forward, 32x32x16 MFMA (variant 2) ------------------------------------------------------
+// Workgroup = 2 waves = 128 query rows of one (pair, head); a wave owns 64 rows = two 32-row
+// q-blocks that share every K / V fragment read (LDS traffic per MFMA half of the 16x16 kernel,
+// and the 32-cycle MFMA leaves 24 issue cycles of VALU beside it instead of 8).
+//  S^T = K Q^T per 32-key block: A = K rows (ds_read_b128), B = Q^T (registers for the whole
+//  sweep). The accumulator has the query on the lane (l & 31) and 16 of the block's keys in its
+//  registers (key (j & 3) + 8 (j >> 2) + 4 (l >> 5) for register j), so the online softmax is
+//  in-lane; the two lane halves hold disjoint keys of the same query and only meet when the
+//  running max moves (lazy rescale, threshold 8 in log2 units) and at the end (row sum).
+//  P^T is the bf16-packed accumulator itself: registers 8s'..8s'+7 are the B operand of k-step s'
+//  of O^T = V^T P^T (guide §3 'An accumulator tile as the next MFMA's operand'); the A operand
+//  V^T is read by ds_read_b64_tr_b16 in that permuted key order.
+// LDS image per tile and operand: [64 keys][64 dims] bf16, 128-B rows, 16-B chunk c of row r at
+// c ^ g((r >> 1) & 7), g(x) = ((x & 1) << 2) | (x >> 1): the b128 K-row reads (16-lane groups of
+// 16 distinct rows) and the transposed V reads (rows r and r + 2 in different 64-B halves) are
+// both conflict-free. The swizzle is applied to the LDS-DMA source.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ uint32_t sign_mask(uint32_t x) {  // x >> 31 arithmetic, opaque
+  uint32_t r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ int sw32(int r) {
+  const int x = (r >> 1) & 7;
+  return ((x & 1) << 2) | (x >> 1);
+}
+__device__ __forceinline__ f32x16 mma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// bf16 B/A fragment from accumulator registers 8s .. 8s + 7
+__device__ __forceinline__ bf16x8_t pack8(const f32x16& x, int s) {
+  u16x8 v = {f2bf(x[8 * s + 0]), f2bf(x[8 * s + 1]), f2bf(x[8 * s + 2]), f2bf(x[8 * s + 3]),
+             f2bf(x[8 * s + 4]), f2bf(x[8 * s + 5]), f2bf(x[8 * s + 6]), f2bf(x[8 * s + 7])};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// DMODE: dropout 0 none, 1 counter hash, 2 counter hash + keep bits out; WIDE: dropout pair
+// indices reach 2^32 (the low word can wrap inside a tile)
+template <int DMODE, bool WIDE>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd32_kernel(AttnArgs a) {
+  constexpr bool DROP = DMODE != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
+  const int T = a.T;
+  const int nkt = (T + 63) >> 6;
+  float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
+  int* sZero = reinterpret_cast<int*>(sBias + nkt * 64);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, r32 = lane & 31;
+  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const int h = bi.h, p = bi.p;
+  const int qw = bi.x * 128 + wave * 64;
+  const int nqb = qw < T ? min(2, (T - qw + 31) >> 5) : 0;  // wave-uniform
+  const int64_t ld = a.ld_qkv;
+  const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
+  const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
+  // LDS-DMA piece = 8 rows x 128 B; lane -> row 8 pc + (lane >> 3), stored chunk lane & 7, source
+  // chunk (lane & 7) ^ g(4 (pc & 1) + (lane >> 4))
+  uint32_t soff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int x = 4 * par + (lane >> 4);
+    const int g = ((x & 1) << 2) | (x >> 1);
+    soff[par] = (uint32_t)((lane >> 3) * ld * 2 + (((lane & 7) ^ g) << 4));
+  }
+  auto stage = [&](int t) {
+    unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int pc = wave * 4 + e;
+      const uint32_t vo = soff[pc & 1] + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2);
+      dma16(rk, kimg + pc * 512, vo);
+      dma16(rv, kimg + IMG + pc * 512, vo);
+    }
+  };
+  stage(0);
+  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+  const float inv_scale = 1.0f / a.scale;
+  for (int tt = wave; tt < nkt; tt += 2) {
+    const int k = tt * 64 + lane;
+    const float bv = k < T ? (kbias ? kbias[k] * inv_scale : 0.f) : -1e30f;
+    sBias[k] = bv;
+    const bool z = __ballot(bv != 0.f) == 0;
+    if (lane == 0) sZero[tt] = z;
+  }
+  // Q^T fragments (B operand): lane (r32, hh) of q-block qb, k-step s: Q[row][16 s + 8 hh ..]
+  const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
+                             a.q_off + h * 64;
+  bf16x8_t qf[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qw + qb * 32 + r32;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (q < T) v = *reinterpret_cast<const u16x8*>(Qb + (int64_t)q * ld + 16 * s + 8 * hh);
+      qf[qb][s] = __builtin_bit_cast(bf16x8_t, v);
+      settle(qf[qb][s]);
+    }
+  }
+  // fragment offsets (elements): K rows kb * 32 + r32 (+ 2048 kb), chunk 2 s + hh
+  const int sw = sw32(r32);
+  int koff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = r32 * 64 + (((2 * s + hh) ^ sw) << 3);
+  // V^T: read e of k-step s (+ 1024 s), d-block db: lane 4q + pp of its 16-lane group addresses
+  // key row 8 e + 4 hh + q, columns 32 db + 16 gi + 4 pp
+  int voff[2][2];
+  {
+    const int gi = (lane >> 4) & 1, q4 = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int r = 8 * e + 4 * hh + q4;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int ch = db * 4 + gi * 2 + (pp >> 1);
+        voff[e][db] = r * 64 + ((ch ^ sw32(r)) << 3) + 4 * (pp & 1);
+      }
+    }
+  }
+  const float c = a.scale * LOG2E;
+  const int Tp2 = (T + 1) & ~1;
+  const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + ((int64_t)p * a.heads + h) * T * a.nkt2,
+                                              (int64_t)T * a.nkt2 * 8)
+                                  : make_rsrc(a.qkv, 0);
+
+  f32x16 o[2][2];
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o[qb][db][j] = 0.f;
+
+  for (int t = 0; t < nkt; ++t) {
+    // tile t landed everywhere (counted wait: a DMODE-2 wave's keep-bit stores of tile t - 1 are
+    // newer than tile t's DMA); buffer (t + 1) & 1 no longer read
+    if (DMODE == 2 && t > 0 && nqb > 0)
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 1 < nkt) stage(t + 1);
+    if (nqb == 0) continue;
+    const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+    const unsigned short* vimg = kimg + IMG;
+    const bool zb = __builtin_amdgcn_readfirstlane(sZero[t]) != 0;
+    // One code path for every tile: the last tile's keys >= T carry a -1e30 bias and the tail
+    // wave's rows >= T have Q = 0 (their outputs are not stored), so nothing is bounds-checked.
+    // S^T for both q-blocks (the K fragments die after these MFMAs)
+    f32x16 sc[2][2];
+    {
+      bf16x8_t kf[2][4];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[kb][s] = lds_row(kimg, kb * 2048 + koff[s]);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          sc[qb][kb] = mma32(kf[kb][0], qf[qb][0], (f32x16){});  // C = inline 0
+#pragma unroll
+          for (int s = 1; s < 4; ++s) sc[qb][kb] = mma32(kf[kb][s], qf[qb][s], sc[qb][kb]);
+        }
+    }
+    if (!zb) {  // additive key mask, stored in raw-score units (bias / scale)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const f32x4 b = *reinterpret_cast<const f32x4*>(sBias + t * 64 + kb * 32 + 8 * jj + 4 * hh);
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[qb][kb][4 * jj + r] += b[r];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the V reads behind the K fragments' last use
+    // V^T fragments, issued now and consumed after the softmax
+    bf16x8_t vf[2][4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (MMSEQ_LDS s16x4*)(vimg + s * 1024 + voff[0][db]));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (MMSEQ_LDS s16x4*)(vimg + s * 1024 + voff[1][db]));
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        vf[db][s] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -1e30f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sc[qb][kb][j]);
+      mx *= c;  // c > 0
+      // lazy rescaling: the running max (shared by the two lane halves of a query) only moves
+      // when some row's tile max exceeds it by more than 8 (log2 units)
+      if (__ballot(mx > m[qb] + 8.f) != 0) {
+        const float mfull = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[qb], mfull);
+        const float alpha = ex2(m[qb] - mn);
+        m[qb] = mn;
+        l[qb] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) o[qb][db] *= alpha;
+      }
+      const float nm = -m[qb];
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float e = ex2(fmaf(sc[qb][kb][j], c, nm));
+          sc[qb][kb][j] = e;
+          rs += e;
+        }
+      l[qb] += rs;
+      if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax)
+        const int q = qw + qb * 32 + r32;
+        // pair index (row base + key) / 2 = dp2 + key / 2: the row base is even and key / 2 < 32,
+        // so the low word never wraps when WIDE is false (checked on the host), and otherwise
+        // the high word takes the carry
+        const uint64_t dp2 = ((((uint64_t)p * a.heads + h) * T + q) * Tp2 + t * 64) >> 1;
+        const uint32_t dlo = (uint32_t)dp2, dhi = (uint32_t)(dp2 >> 32);
+        const uint32_t H0 = dhi ^ a.drop.k1, H1 = (dhi + 1u) ^ a.drop.k1;
+        const uint32_t thr = a.drop.thr;
+        uint32_t wb[2] = {0u, 0u};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int j = 0; j < 16; j += 2) {
+            const int key = kb * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;  // even
+            const uint32_t lo = dlo + (uint32_t)(key >> 1);
+            const uint32_t hw = WIDE ? (lo < dlo ? H1 : H0) : H0;
+            const uint32_t hs = drop_mix((lo ^ a.drop.k0) + hw);  // = drop_hash(pair index)
+            // all-ones where dropped (half < thr), as plain VALU values: the shift is opaque asm so
+            // the compiler cannot turn it into a compare + select (64 lane masks in SGPRs spill)
+            const uint32_t d0 = sign_mask((hs & 0xFFFFu) - thr);
+            const uint32_t d1 = sign_mask((hs >> 16) - thr);
+            sc[qb][kb][j] = __uint_as_float(__float_as_uint(sc[qb][kb][j]) & ~d0);
+            sc[qb][kb][j + 1] = __uint_as_float(__float_as_uint(sc[qb][kb][j + 1]) & ~d1);
+            if (DMODE == 2) {  // bit of key jj: 16 ((jj >> 2) & 3) + 4 (jj >> 4) + (jj & 3)
+              const int pos = 16 * hh + 8 * kb + 4 * (j >> 3) + (j & 3);
+              wb[(j >> 2) & 1] |= ((~d0 & 1u) | (~d1 & 2u)) << pos;
+            }
+          }
+        }
+        if (DMODE == 2) {
+          wb[0] |= __shfl_xor(wb[0], 32, 64);
+          wb[1] |= __shfl_xor(wb[1], 32, 64);
+          // rows q >= T fall outside the descriptor and are dropped; lane half 1 stores nothing
+          const uint32_t bo = (uint32_t)((q * a.nkt2 + t) * 8);
+          __builtin_amdgcn_raw_buffer_store_b32(wb[0], rbits, hh ? 0xFFFFFFF0u : bo, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(wb[1], rbits, hh ? 0xFFFFFFF0u : bo + 4, 0, 0);
+        }
+      }
+    }
+    // O^T += V^T P^T (P^T = the bf16-packed score registers)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const bf16x8_t pf = pack8(sc[qb][s >> 1], s & 1);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) o[qb][db] = mma32(vf[db][s], pf, o[qb][db]);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nqb == 0) return;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    if (qb >= nqb) break;
+    const float lt = l[qb] + __shfl_xor(l[qb], 32, 64);
+    const int q = qw + qb * 32 + r32;
+    if (q < T) {
+      const float inv = (DROP ? a.drop.scale : 1.0f) / lt;
+      unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
+                           h * 64 + 4 * hh;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const f32x4 v = {o[qb][db][4 * jj], o[qb][db][4 * jj + 1], o[qb][db][4 * jj + 2],
+                           o[qb][db][4 * jj + 3]};
+          Vec4<unsigned short>::st(op + db * 32 + 8 * jj, v * inv);
+        }
+      if (hh == 0) a.lse[((int64_t)p * a.heads + h) * T + q] = (m[qb] + __builtin_amdgcn_logf(lt)) * LN2;
+    }
+  }
+}
+
 // ---- backward: dQ (per 128-query block, keys swept), also writes delta = rowsum(dO * O) --------
 template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
 __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
@@ -1204,7 +1504,24 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   a.drop = make_drop(drop);
   dim3 grid((T + QT - 1) / QT, heads, P);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (dtype == MMSEQ_BF16 && variant) {
+  if (dtype == MMSEQ_BF16 && variant == 2) {
+    MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
+    const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
+    const int nkt = (T + 63) / 64;
+    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)nkt * (64 + 1) * 4;
+    a.bits = keep_bits;
+    a.nkt2 = (nkt + 1) & ~1;
+    // largest dropout pair index + the in-tile key offset must stay below 2^32 for the narrow path
+    const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 1) & ~1)) / 2 + 64 >= (1ull << 32);
+    if (a.drop.thr && keep_bits)
+      hipLaunchKernelGGL((wide ? attn_fwd32_kernel<2, true> : attn_fwd32_kernel<2, false>), gq,
+                         dim3(128), lds, s, a);
+    else if (a.drop.thr)
+      hipLaunchKernelGGL((wide ? attn_fwd32_kernel<1, true> : attn_fwd32_kernel<1, false>), gq,
+                         dim3(128), lds, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd32_kernel<0, false>), gq, dim3(128), lds, s, a);
+  } else if (dtype == MMSEQ_BF16 && variant) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;

@@ -197,12 +197,14 @@ __host__ inline Drop make_drop(const mmseq_dropout* d) {
   }
   return r;
 }
-__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t pair) {
-  // high word enters by xor + add (no multiply: pair indices here stay below 2^32, and the
-  // lowbias32 rounds below provide the diffusion)
-  uint32_t x = ((uint32_t)pair ^ d.k0) + ((uint32_t)(pair >> 32) ^ d.k1);
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {  // Wellons' lowbias32
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
+}
+__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t pair) {
+  // high word enters by xor + add (no multiply: pair indices here stay below 2^32, and the
+  // lowbias32 rounds provide the diffusion)
+  return drop_mix(((uint32_t)pair ^ d.k0) + ((uint32_t)(pair >> 32) ^ d.k1));
 }
 __device__ __forceinline__ float drop_sel(const Drop& d, uint32_t h, int hi) {
   const uint32_t u = hi ? (h >> 16) : (h & 0xFFFFu);

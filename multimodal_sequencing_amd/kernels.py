@@ -108,8 +108,10 @@ class LayerRefs:
 # ================================================================================================
 class BertLayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps, drops=(None, None, None)):
-        """drops = (attention probs :419, self-output dense :437, output dense :491)."""
+    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps, drops=(None, None, None), save=True):
+        """drops = (attention probs :419, self-output dense :437, output dense :491); save=False
+        (the caller runs under no_grad) skips the stores only the backward reads (GELU
+        pre-activation)."""
         st = L.store
         H = x.shape[-1]
         d_att, d_o, d_out = drops
@@ -119,7 +121,7 @@ class BertLayerFn(torch.autograd.Function):
         o = torch.empty_like(x)
         lse = torch.empty(P, heads, T, device=x.device)
         # the forward's dropout keep mask as bits (1 bit per score; read back by the backward)
-        kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None else None
+        kbits = (N.attn_keep_bits(P, T, heads, x.device) if d_att is not None and save else None)
         N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
                    H, lse, drop=d_att, keep_bits=kbits)
         s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, drop=d_o)
@@ -128,7 +130,8 @@ class BertLayerFn(torch.autograd.Function):
         r1 = torch.empty_like(m1)
         N.layernorm_fwd(s1.shape[0], H, s1, _rows(H), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, h1,
                         _rows(H), m1, r1)
-        z = torch.empty(x.shape[0], st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype)
+        z = (torch.empty(x.shape[0], st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype)
+             if save else None)
         gact = _linear(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU, aux=z)
         s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1, drop=d_out)
         y = torch.empty_like(x)
@@ -136,6 +139,8 @@ class BertLayerFn(torch.autograd.Function):
         r2 = torch.empty_like(m1)
         N.layernorm_fwd(s2.shape[0], H, s2, _rows(H), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y,
                         _rows(H), m2, r2)
+        if not save:
+            return y
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
         ctx.meta = (L, P, T, heads, drops)
         ctx.kbits = kbits
@@ -179,7 +184,7 @@ class BertLayerFn(torch.autograd.Function):
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         st.grad_ready(L.span)
         dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
-        return dx, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None
 
 
 # ================================================================================================
@@ -187,7 +192,7 @@ class BertLayerFn(torch.autograd.Function):
 # ================================================================================================
 class VitBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, anchor, L, P, T, heads, eps):
+    def forward(ctx, h, anchor, L, P, T, heads, eps, save=True):
         st = L.store
         W = h.shape[-1]
         R = h.shape[0]
@@ -207,9 +212,11 @@ class VitBlockFn(torch.autograd.Function):
         hn2 = torch.empty_like(h)
         N.layernorm_fwd(R, W, x1, _rows(W), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, hn2, _rows(W),
                         m2, r2)
-        z = torch.empty(R, st.w(L.fc_w).shape[0], device=h.device, dtype=h.dtype)
+        z = torch.empty(R, st.w(L.fc_w).shape[0], device=h.device, dtype=h.dtype) if save else None
         gact = _linear(hn2, st.w(L.fc_w), bias=st.f32(L.fc_b), act=QGELU, aux=z)
         x2 = _linear(gact, st.w(L.proj_w), bias=st.f32(L.proj_b), resid=x1)
+        if not save:
+            return x2
         ctx.save_for_backward(h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact)
         ctx.meta = (L, P, T, heads)
         return x2
@@ -243,7 +250,7 @@ class VitBlockFn(torch.autograd.Function):
         N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
                         dx1, _rows(W), st.g(L.ln1_w), st.g(L.ln1_b))
         st.grad_ready(L.span)
-        return dh, None, None, None, None, None, None
+        return dh, None, None, None, None, None, None, None
 
 
 # ================================================================================================

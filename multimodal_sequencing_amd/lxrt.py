@@ -217,8 +217,9 @@ class LXRTModel(nn.Module):
         Tv = 1 + 2 * g * g
         cd = st.compute_dtype
         h = K.VitStemFn.apply(images, pairs_list, self._anchor, self.stem_refs, patch, 1e-5, cd)
+        save = torch.is_grad_enabled()
         for L in self.block_refs:
-            h = K.VitBlockFn.apply(h, self._anchor, L, P, Tv, heads, 1e-5)
+            h = K.VitBlockFn.apply(h, self._anchor, L, P, Tv, heads, 1e-5, save)
         return K.VitProjFn.apply(h, self._anchor, self.proj_refs), Tv
 
     def encode_joint(self, input_ids, attention_mask, token_type_ids=None, images=None,
@@ -245,10 +246,11 @@ class LXRTModel(nn.Module):
                                            Tv, 1e-12, st.compute_dtype,
                                            (D.site(ph, "emb"), D.site(ph, "visn_fc")))
         heads = self.config.num_attention_heads
+        save = torch.is_grad_enabled()
         for i, L in enumerate(self.layer_refs):
             x = K.BertLayerFn.apply(x, key_bias, self._anchor, L, P, T, heads, 1e-12,
                                     (D.site(pa, "att", i), D.site(ph, "att_out", i),
-                                     D.site(ph, "out", i)))
+                                     D.site(ph, "out", i)), save)
         return x.view(P, T, -1), Lt
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, visual_feats=None,

@@ -105,7 +105,10 @@ def test_layernorm_dropout_fwd_bwd(dtype):
 @pytest.mark.parametrize("P,T,heads,masked", [(2, 129, 2, True), (1, 513, 3, True),
                                               (2, 64, 1, False), (1, 200, 2, False)])
 @pytest.mark.parametrize("bits", [False, True])
-def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked, bits):
+@pytest.mark.parametrize("fast", [1, 2])
+def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked, bits, fast):
+    if fast == 2 and dtype == torch.float32:
+        pytest.skip("variant 2 is a bf16 forward")
     g = torch.Generator(device="cpu").manual_seed(T + heads)
     H = heads * 64
     qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, dtype)
@@ -119,7 +122,9 @@ def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked, bits):
     out = torch.empty(P * T, H, device=DEV, dtype=dtype)
     lse = torch.empty(P, heads, T, device=DEV)
     kb = nat.attn_keep_bits(P, T, heads, DEV) if bits else None
+    nat.attn_set_fast(fast)
     nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse, drop=d, keep_bits=kb)
+    nat.attn_set_fast(1)
     Tp2 = (T + 1) & ~1  # attention mask rows are laid out with an even stride
     Mk = _mask((P, heads, T, Tp2), d)[..., :T]
     qf = qkv.float().requires_grad_(True)

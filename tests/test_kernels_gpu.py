@@ -147,7 +147,7 @@ def _attn_ref(qkv, P, T, heads, bias, scale):
 @pytest.mark.parametrize("P,T,heads,masked", [(2, 64, 1, False), (3, 129, 2, True), (2, 33, 2, True),
                                               (1, 513, 12, True), (2, 393, 2, False), (1, 1, 1, False),
                                               (2, 127, 1, True)])
-@pytest.mark.parametrize("fast", [1, 0])
+@pytest.mark.parametrize("fast", [1, 0, 2])
 def test_attention_fwd_bwd(dtype, P, T, heads, masked, fast):
     nat.attn_set_fast(fast)
     g = torch.Generator(device="cpu").manual_seed(P * T + heads)
@@ -177,7 +177,8 @@ def test_attention_fwd_bwd(dtype, P, T, heads, masked, fast):
 
 @pytest.mark.parametrize("profile", ["ramp_up", "ramp_down", "jump"])
 @pytest.mark.parametrize("bias_mode", ["none", "first_tile_masked", "zeros"])
-def test_attention_rescale_and_zero_bias_tiles(profile, bias_mode):
+@pytest.mark.parametrize("fast", [1, 2])
+def test_attention_rescale_and_zero_bias_tiles(profile, bias_mode, fast):
     """bf16 fast kernels: the running max moves only when a row's tile max exceeds it by > 8
     (log2) and all-zero-bias key tiles skip the bias add. Scores that climb across key tiles
     (several rescales mid-sequence), fall (none after the first tile) or jump, with a key bias
@@ -209,7 +210,9 @@ def test_attention_rescale_and_zero_bias_tiles(profile, bias_mode):
     scale = 1 / 8
     out = torch.empty(P * T, H, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(P, heads, T, device=DEV)
+    nat.attn_set_fast(fast)
     nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse)
+    nat.attn_set_fast(1)
     qf = qkv.float().requires_grad_(True)
     ref = _attn_ref(qf, P, T, heads, bias, scale)
     _close(out, ref, torch.bfloat16)

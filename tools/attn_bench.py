@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodal_sequencing_amd import _native as N
 
 
-def run(P, T, heads, drop, iters=5, bits=False):
+def run(P, T, heads, drop, iters=5, bits=False, variant=1):
     H = heads * 64
     g = torch.Generator(device="cpu").manual_seed(0)
     qkv = (torch.randn(P * T, 3 * H, generator=g) * 0.5).to("cuda", torch.bfloat16)
@@ -22,6 +22,7 @@ def run(P, T, heads, drop, iters=5, bits=False):
     bwd = lambda: N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, dout, H,
                              lse, delta, dqkv, 3 * H, drop=d, keep_bits=kb)
     res = {}
+    N.attn_set_fast(variant)
     for name, f in (("fwd", fwd), ("bwd", bwd)):
         f(); torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -35,7 +36,9 @@ def run(P, T, heads, drop, iters=5, bits=False):
     return res
 
 
-for P, T in ((320, 513), (320, 393)):
-    for drop, bits in ((False, False), (True, False), (True, True)):
-        print(json.dumps({"P": P, "T": T, "drop": drop, "bits": bits, **run(P, T, 12, drop, bits=bits)}),
-              flush=True)
+variants = [int(v) for v in sys.argv[1:]] or [1, 2]
+for P, T in ((320, 513), (320, 393), (320, 512)):
+    for drop, bits in ((False, False), (True, True)):
+        for var in variants:
+            print(json.dumps({"P": P, "T": T, "drop": drop, "bits": bits, "variant": var,
+                              **run(P, T, 12, drop, bits=bits, variant=var)}), flush=True)

@@ -9,6 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodal_sequencing_amd import _native as N  # noqa: E402
 
 P, heads = 320, 12
+N.attn_set_fast(int(os.environ.get("ATTN_VARIANT", "2")))
 H = heads * 64
 for T in [int(x) for x in sys.argv[1:]]:
     g = torch.Generator(device="cpu").manual_seed(0)
