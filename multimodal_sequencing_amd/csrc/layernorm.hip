@@ -4,12 +4,12 @@
 // Rows are addressed through mmseq_rows (two-level strides) so the kernels can read / write the
 // text or the visual half of the joint [P][T][H] activation in place (the fused concat).
 // Lane l owns columns j*256 + 4l .. +3 (j < 4): 8-byte (bf16) / 16-byte (f32) accesses when the
-// row layout allows it (VEC), scalar otherwise; cols <= 1024.
+// row layout allows it (VEC), scalar otherwise; cols <= 256 * MJ (MJ = 4 up to 1024 columns, 8 up
+// to 2048: the 2H-wide MRM head LayerNorm of the pretraining path).
 #include "common.h"
 
 namespace {
 
-constexpr int MAXJ = 4;   // 4 x 256 columns
 constexpr int RPB = 128;  // rows per workgroup in bwd (dgamma/dbeta partial granularity)
 
 // 32-bit division (rows < 2^31): a 64-bit divide is a ~100-instruction branchy subroutine
@@ -47,7 +47,7 @@ __device__ __forceinline__ f32x4 ldp(const float* p, int c, int cols) {
   return v;
 }
 
-template <typename TX, typename TY, bool VEC>
+template <typename TX, typename TY, bool VEC, int MAXJ>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const TX* __restrict__ x,
                                                      mmseq_rows xl, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
 
 // dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres)
 // per-block partial dgamma / dbeta -> ws[block][2][cols]
-template <typename T, bool VEC>
+template <typename T, bool VEC, int MAXJ>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                      mmseq_rows dyl, const T* __restrict__ x,
                                                      mmseq_rows xl, const float* __restrict__ mean,
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
                                                      const T* __restrict__ dres, mmseq_rows dresl,
                                                      float* __restrict__ ws, Drop din,
                                                      T* __restrict__ dxd, Drop dout) {
-  __shared__ float red[4][2][1024];
+  __shared__ float red[4][2][256 * MAXJ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4 pg[MAXJ], pb[MAXJ], gm[MAXJ];
 #pragma unroll
@@ -419,7 +419,7 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
                                             void* y, mmseq_rows yl, float* mean, float* rstd,
                                             mmseq_dtype xd, mmseq_dtype yd,
                                             const mmseq_dropout* drop_y, mmseq_stream stream) {
-  MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 1024, "layernorm: cols must be in (0, 1024]");
+  MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 2048, "layernorm: cols must be in (0, 2048]");
   MMSEQ_REQUIRE(x && y && gamma && beta, "layernorm: null buffer");
   MMSEQ_REQUIRE(xl.rpb > 0 && yl.rpb > 0, "layernorm: rpb must be > 0");
   if (rows == 0) return MMSEQ_OK;
@@ -428,7 +428,7 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
   const bool vec = cols % 4 == 0 && rows_vec(x, xl, xd == MMSEQ_BF16 ? 2 : 4) &&
                    rows_vec(y, yl, yd == MMSEQ_BF16 ? 2 : 4);
   const Drop dd = make_drop(drop_y);
-  if (xd == MMSEQ_BF16 && yd == MMSEQ_BF16 && cols % 256 == 0 && rows_vec16(x, xl) &&
+  if (xd == MMSEQ_BF16 && yd == MMSEQ_BF16 && cols % 256 == 0 && cols <= 1024 && rows_vec16(x, xl) &&
       rows_vec16(y, yl) && ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0) {
     const dim3 g8((rows + 7) / 8);
     switch (cols / 256) {
@@ -439,11 +439,15 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
     }
     return mmseq_check_launch("layernorm_fwd");
   }
-#define LNF(TX, TY, V)                                                                           \
-  hipLaunchKernelGGL((ln_fwd_kernel<TX, TY, V>), grid, dim3(256), 0, s, rows, cols, (const TX*)x, \
-                     xl, gamma, beta, eps, (TY*)y, yl, mean, rstd, dd)
+#define LNF(TX, TY, V)                                                                            \
+  if (cols <= 1024)                                                                               \
+    hipLaunchKernelGGL((ln_fwd_kernel<TX, TY, V, 4>), grid, dim3(256), 0, s, rows, cols,           \
+                       (const TX*)x, xl, gamma, beta, eps, (TY*)y, yl, mean, rstd, dd);            \
+  else                                                                                            \
+    hipLaunchKernelGGL((ln_fwd_kernel<TX, TY, V, 8>), grid, dim3(256), 0, s, rows, cols,           \
+                       (const TX*)x, xl, gamma, beta, eps, (TY*)y, yl, mean, rstd, dd)
 #define LNF2(TX, TY) \
-  if (vec) LNF(TX, TY, true); else LNF(TX, TY, false)
+  if (vec) { LNF(TX, TY, true); } else { LNF(TX, TY, false); }
   if (xd == MMSEQ_F32 && yd == MMSEQ_F32) { LNF2(float, float); }
   else if (xd == MMSEQ_F32 && yd == MMSEQ_BF16) { LNF2(float, unsigned short); }
   else if (xd == MMSEQ_BF16 && yd == MMSEQ_F32) { LNF2(unsigned short, float); }
@@ -466,7 +470,7 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
                                             mmseq_dtype dtype, const mmseq_dropout* drop_dy,
                                             void* dx_drop, const mmseq_dropout* drop_dx,
                                             mmseq_stream stream) {
-  MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 1024, "layernorm_bwd: cols must be in (0, 1024]");
+  MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 2048, "layernorm_bwd: cols must be in (0, 2048]");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "layernorm_bwd: null buffer");
   if (rows == 0) return MMSEQ_OK;
   if (!dres) dresl = dxl;
@@ -477,7 +481,7 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
                    rows_vec(dx, dxl, esz) && (!dres || rows_vec(dres, dresl, esz)) &&
                    (!dx_drop || ((uintptr_t)dx_drop % (4 * esz)) == 0);
   const Drop din = make_drop(drop_dy), dout = make_drop(drop_dx);
-  if (dtype == MMSEQ_BF16 && cols % 256 == 0 && rows_vec16(dy, dyl) && rows_vec16(x, xl) &&
+  if (dtype == MMSEQ_BF16 && cols % 256 == 0 && cols <= 1024 && rows_vec16(dy, dyl) && rows_vec16(x, xl) &&
       rows_vec16(dx, dxl) && (!dres || rows_vec16(dres, dresl)) &&
       (!dx_drop || ((uintptr_t)dx_drop % 16) == 0) && ((uintptr_t)gamma % 16) == 0) {
     const int nb16 = (rows + RPB16 - 1) / RPB16;
@@ -501,15 +505,18 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
     if (dgamma || dbeta) return ln_reduce_partials(nb16, cols, workspace, dgamma, dbeta, s);
     return MMSEQ_OK;
   }
-#define LNB(T, V)                                                                                 \
-  hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy,  \
-                     dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl, \
+#define LNBJ(T, V, J)                                                                             \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, V, J>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy, \
+                     dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl,   \
                      workspace, din, (T*)dx_drop, dout)
+#define LNB(T, V) \
+  if (cols <= 1024) { LNBJ(T, V, 4); } else { LNBJ(T, V, 8); }
   if (dtype == MMSEQ_F32) {
-    if (vec) LNB(float, true); else LNB(float, false);
+    if (vec) { LNB(float, true); } else { LNB(float, false); }
   } else {
-    if (vec) LNB(unsigned short, true); else LNB(unsigned short, false);
+    if (vec) { LNB(unsigned short, true); } else { LNB(unsigned short, false); }
   }
+#undef LNBJ
 #undef LNB
   mmseq_status st = mmseq_check_launch("layernorm_bwd");
   if (st) return st;

@@ -47,7 +47,7 @@ class LXRTConfig(SimpleNamespace):
                          attention_probs_dropout_prob=attention_probs_dropout_prob, **kw)
 
 
-def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25):
+def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25, img_part=False):
     H, I = cfg.hidden_size, cfg.intermediate_size
     std = cfg.initializer_range
     sp = [Spec("embeddings.word_embeddings.weight", (cfg.vocab_size, H), normal(std)),
@@ -62,7 +62,8 @@ def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25):
         sp += ln_specs("encoder.visn_fc.visn_layer_norm", H)
         sp += linear_specs("encoder.visn_fc.box_fc", 4, H, std=std, transpose=False)
         sp += ln_specs("encoder.visn_fc.box_layer_norm", H)
-    for i in range(cfg.num_hidden_layers):
+    # the image-only model (multimodal_img_part) builds no BertLayer stack (lxrt:797-798)
+    for i in range(0 if img_part else cfg.num_hidden_layers):
         b = f"encoder.layer.{i}."
         a = b + "attention.self."
         sp += [Spec(a + "query.weight", (H, H), normal(std), transpose=True, pack=f"qkvw{i}"),
@@ -120,17 +121,19 @@ class LXRTModel(nn.Module):
                  clip_model_name="ViT-B/16", num_labels=None, device="cuda",
                  compute_dtype=torch.bfloat16, vision=None, **kw):
         super().__init__()
-        if multimodal_img_part:
-            raise NotImplementedError("image-only pretraining (config 2) is a 'next' row (SURVEY §8f)")
+        if multimodal_img_part and multimodal_text_part:
+            raise ValueError("multimodal_img_part and multimodal_text_part are exclusive")
         if num_labels is not None:
             raise NotImplementedError("topological-sort head is out of scope (SURVEY §2 row 3)")
         self.config = config
         self.text_part = multimodal_text_part
+        self.img_part = multimodal_img_part
         self.cls_id, self.sep_id = cls_id, sep_id
         self.clip_model_name = clip_model_name
         self.vision = dict(vision or CLIP_VISION[clip_model_name])
         self.img_len = 2  # VISUAL_CONFIG.max_subsample_image_length for BERSON input (lxrt:770)
-        specs = _lxrt_specs(config, self.vision, multimodal_text_part, max_story_length)
+        specs = _lxrt_specs(config, self.vision, multimodal_text_part, max_story_length,
+                            img_part=multimodal_img_part)
         self.store = ParamStore(specs, device, compute_dtype)
         self.store.init_weights(seed=kw.get("seed", 0))
         attach_tree(self, self.store.params)
@@ -150,7 +153,7 @@ class LXRTModel(nn.Module):
     def _build_refs(self):
         st = self.store
         self.layer_refs = []
-        for i in range(self.config.num_hidden_layers):
+        for i in range(0 if self.img_part else self.config.num_hidden_layers):
             b = f"encoder.layer.{i}."
             a = b + "attention.self."
             self.layer_refs.append(K.LayerRefs(
