@@ -202,16 +202,18 @@ int64_t mmseq_embed_ln_bwd_workspace(int P, int Lt, int H);
 
 /* ------------------------------------------------------------------------------------------
  * ViT patch path (clip/model.py:262-278 with the img_len=2 quirk).
- *  im2col: images [B][N][3][R][R] f32 + pairs [B][npair][2] -> patches [B*npair][2*g*g][3*ps*ps]
- *          (pair images gathered on device: no 8x duplicated H2D copy, process_images :82-97)
+ *  im2col: images [B][N][3][R][R] f32 + pairs [B][npair][2] -> patches [B*npair][2*g*g] rows of
+ *          ld_patch >= 3*ps*ps elements, columns past 3*ps*ps zero (K padded for the GEMM, e.g.
+ *          588 -> 640 for ViT-L/14) (pair images gathered on device: no 8x duplicated H2D copy,
+ *          process_images :82-97)
  *  embed_fwd: x[p][0] = cls + pos[0]; x[p][1+j] = patch_out[p][j] + pos[j < g*g ? 1+j : j-g*g]
  *             y = LN(x) (ln_pre, eps)   (x saved for bwd as dtype)
  *  embed_bwd: dx = LN'(dy); dcls += sum_p dx[p][0]; dpos[r] += sum of its tokens;
  *             dpatch_out[p][j] = dx[p][1+j]
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_vit_im2col(int B, int N, int npair, int R, int ps, const float* images,
-                              const int64_t* pairs, void* patches, mmseq_dtype dtype,
-                              mmseq_stream stream);
+                              const int64_t* pairs, void* patches, int64_t ld_patch,
+                              mmseq_dtype dtype, mmseq_stream stream);
 mmseq_status mmseq_vit_embed_fwd(int P, int ntok, int W, int npatch_img, const void* patch_out,
                                  const float* cls, const float* pos, const float* gamma,
                                  const float* beta, float eps, void* x, void* y, float* mean,

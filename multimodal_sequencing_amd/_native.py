@@ -91,7 +91,8 @@ _SIGS = {
     "mmseq_embed_ln_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 9 + [_c_i64] + [_vp] * 6 +
                            [ctypes.c_int, _dp, _vp]),
     "mmseq_embed_ln_bwd_workspace": (ctypes.c_int64, [ctypes.c_int] * 3),
-    "mmseq_vit_im2col": (ctypes.c_int, [ctypes.c_int] * 5 + [_vp, _vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_vit_im2col": (ctypes.c_int, [ctypes.c_int] * 5 + [_vp, _vp, _vp, _c_i64, ctypes.c_int,
+                                                             _vp]),
     "mmseq_vit_embed_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float] +
                             [_vp] * 4 + [ctypes.c_int, _vp]),
     "mmseq_vit_embed_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 11 + [ctypes.c_int, _vp]),
@@ -301,8 +302,9 @@ def embed_ln_bwd(P, Lt, H, ids, tt, word, pos, typ, gamma, mean, rstd, djoint, l
 
 
 def vit_im2col(B, N, npair, R, ps, images, pairs, patches):
+    """patches [rows][ld]: ld >= 3 ps^2, the extra columns are zero-filled."""
     _check(lib().mmseq_vit_im2col(B, N, npair, R, ps, _p(images), _p(pairs), _p(patches),
-                                  dt(patches), _stream()), "mmseq_vit_im2col")
+                                  patches.shape[-1], dt(patches), _stream()), "mmseq_vit_im2col")
 
 
 def vit_embed_fwd(P, ntok, W, npatch, patch_out, cls, pos, gamma, beta, eps, x, y, mean, rstd):

@@ -160,32 +160,38 @@ __global__ __launch_bounds__(256) void embed_pos_kernel(int P, int Lt, int H,
 // ---------------------------------------------------------------------------------------------
 // ViT patch path
 // ---------------------------------------------------------------------------------------------
+// Any patch size: one workgroup (64 lanes) per patch row; lane t < 3 ps copies the ps pixels of
+// (channel t / ps, kernel row t % ps) — contiguous in the image — and the columns K .. ldk - 1 are
+// zero-filled (K padded to the GEMM's K granularity, e.g. 588 -> 640 for ViT-L/14).
 template <typename T>
-__global__ __launch_bounds__(256) void im2col_kernel(int B, int N, int npair, int R, int ps,
-                                                     const float* __restrict__ images,
-                                                     const int64_t* __restrict__ pairs,
-                                                     T* __restrict__ out) {
+__global__ __launch_bounds__(64) void im2col_kernel(int64_t rows, int N, int npair, int R, int ps,
+                                                    int64_t ldk, const float* __restrict__ images,
+                                                    const int64_t* __restrict__ pairs,
+                                                    T* __restrict__ out) {
   const int g = R / ps, gg = g * g, K = 3 * ps * ps;
-  const int64_t total = (int64_t)B * npair * 2 * gg * K;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * 256) {
-    int col = e % K;
-    int64_t row = e / K;  // (b*npair + j)*2*gg + s*gg + patch
-    int patch = row % gg;
-    int s = (row / gg) % 2;
-    int64_t pj = row / (2 * gg);
-    int b = pj / npair, j = pj % npair;
-    int img = (int)pairs[((int64_t)b * npair + j) * 2 + s];
-    int c = col / (ps * ps), ky = (col / ps) % ps, kx = col % ps;
-    int py = patch / g, px = patch % g;
-    float v = images[((((int64_t)b * N + img) * 3 + c) * R + py * ps + ky) * R + px * ps + kx];
-    Elem<T>::st(out + e, v);
+  const int64_t row = blockIdx.x;
+  if (row >= rows) return;
+  const int patch = (int)(row % gg);
+  const int64_t rest = row / gg;
+  const int s = (int)(rest & 1);
+  const int64_t pj = rest >> 1;
+  const int b = (int)(pj / npair);
+  const int img = (int)pairs[pj * 2 + s];
+  const int py = patch / g, px = patch % g;
+  const float* src_img = images + ((int64_t)b * N + img) * 3 * R * R;
+  T* dst = out + row * ldk;
+  for (int t = threadIdx.x; t < 3 * ps; t += 64) {
+    const int c = t / ps, ky = t % ps;
+    const float* src = src_img + ((int64_t)c * R + py * ps + ky) * R + px * ps;
+    T* d = dst + (c * ps + ky) * ps;
+    for (int kx = 0; kx < ps; ++kx) Elem<T>::st(d + kx, src[kx]);
   }
+  for (int col = K + threadIdx.x; col < ldk; col += 64) Elem<T>::st(dst + col, 0.f);
 }
 
 // bf16 patches: one row per 96 threads, 8 consecutive pixels of one (channel, patch row) per
 // thread (two 16-byte loads, one 16-byte store); the row's pair / image decode is done once
-// per row instead of per element (64-bit divisions). Requires ps % 8 == 0.
+// per row instead of per element (64-bit divisions). Requires ps % 8 == 0 and ldk == K.
 __global__ __launch_bounds__(192) void im2col_bf16_kernel(int64_t rows, int N, int npair, int R,
                                                          int ps, const float* __restrict__ images,
                                                          const int64_t* __restrict__ pairs,
@@ -444,25 +450,25 @@ extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* 
 
 extern "C" mmseq_status mmseq_vit_im2col(int B, int N, int npair, int R, int ps,
                                          const float* images, const int64_t* pairs, void* patches,
-                                         mmseq_dtype dtype, mmseq_stream stream) {
+                                         int64_t ld_patch, mmseq_dtype dtype, mmseq_stream stream) {
   MMSEQ_REQUIRE(B >= 0 && N > 0 && npair > 0 && ps > 0 && R % ps == 0, "im2col: bad sizes");
   MMSEQ_REQUIRE(images && pairs && patches, "im2col: null buffer");
+  MMSEQ_REQUIRE(ld_patch >= 3 * ps * ps, "im2col: ld_patch < 3 ps^2");
   if (B == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t total = (int64_t)B * npair * 2 * (R / ps) * (R / ps) * 3 * ps * ps;
-  const int64_t blocks = (total + 255) / 256;
-  dim3 grid((unsigned)(blocks < 65536 ? blocks : 65536));
-  if (dtype == MMSEQ_F32)
-    hipLaunchKernelGGL(im2col_kernel<float>, grid, dim3(256), 0, s, B, N, npair, R, ps, images,
-                       pairs, (float*)patches);
-  else if (ps % 8 == 0 && R % 4 == 0 && (((uintptr_t)images) & 15) == 0 &&
-           (((uintptr_t)patches) & 15) == 0) {
-    const int64_t rows = (int64_t)B * npair * 2 * (R / ps) * (R / ps);
+  const int64_t rows = (int64_t)B * npair * 2 * (R / ps) * (R / ps);
+  MMSEQ_REQUIRE(rows < (1ll << 31), "im2col: too many patches");
+  if (dtype == MMSEQ_BF16 && ps % 8 == 0 && R % 4 == 0 && ld_patch == 3 * ps * ps &&
+      (((uintptr_t)images) & 15) == 0 && (((uintptr_t)patches) & 15) == 0) {
     hipLaunchKernelGGL(im2col_bf16_kernel, dim3((unsigned)((rows + 1) / 2)), dim3(192), 0, s, rows, N,
                        npair, R, ps, images, pairs, (unsigned short*)patches);
-  } else
-    hipLaunchKernelGGL(im2col_kernel<unsigned short>, grid, dim3(256), 0, s, B, N, npair, R, ps,
-                       images, pairs, (unsigned short*)patches);
+  } else if (dtype == MMSEQ_F32) {
+    hipLaunchKernelGGL(im2col_kernel<float>, dim3((unsigned)rows), dim3(64), 0, s, rows, N, npair,
+                       R, ps, ld_patch, images, pairs, (float*)patches);
+  } else {
+    hipLaunchKernelGGL(im2col_kernel<unsigned short>, dim3((unsigned)rows), dim3(64), 0, s, rows, N,
+                       npair, R, ps, ld_patch, images, pairs, (unsigned short*)patches);
+  }
   return mmseq_check_launch("vit_im2col");
 }
 

@@ -257,6 +257,14 @@ class VitBlockFn(torch.autograd.Function):
 # ViT stem: pair-image gather + patchify GEMM + class token + positional quirk + ln_pre
 # ================================================================================================
 class VitStemFn(torch.autograd.Function):
+    """conv1 (k = s = patch, no bias) as im2col + GEMM. K = 3 p^2 is padded to the GEMM's
+    128-element granularity when it is not a multiple of it (ViT-L/14: 588 -> 640, zero columns in
+    the patches and the weight operand), so every patch size takes the MFMA kernels."""
+
+    @staticmethod
+    def kpad(K):
+        return K if K % 128 == 0 else (K + 127) // 128 * 128
+
     @staticmethod
     def forward(ctx, images, pairs, anchor, L, patch, eps, cdtype):
         st = L.store
@@ -268,8 +276,14 @@ class VitStemFn(torch.autograd.Function):
         ntok = 1 + 2 * gg
         Wc = st.w(L.conv_w)  # [W][3][p][p] -> [W][3p^2]
         W = Wc.shape[0]
-        Wc = Wc.reshape(W, -1)
-        patches = torch.empty(P * 2 * gg, 3 * patch * patch, device=images.device, dtype=cdtype)
+        K = 3 * patch * patch
+        Kp = VitStemFn.kpad(K)
+        Wc = Wc.reshape(W, K)
+        if Kp != K:
+            Wp = torch.zeros(W, Kp, device=images.device, dtype=cdtype)
+            Wp[:, :K] = Wc
+            Wc = Wp
+        patches = torch.empty(P * 2 * gg, Kp, device=images.device, dtype=cdtype)
         N.vit_im2col(B, Nst, npair, R_, patch, images, pairs, patches)
         po = _linear(patches, Wc)
         del patches
@@ -292,9 +306,12 @@ class VitStemFn(torch.autograd.Function):
         dpo = torch.empty(P * (ntok - 1), W, device=x0.device, dtype=cdtype)
         N.vit_embed_bwd(P, ntok, W, gg, dh0.contiguous(), x0, mean, rstd, st.f32(L.ln_w), dpo,
                         st.g(L.cls), st.g(L.pos), st.g(L.ln_w), st.g(L.ln_b))
-        patches = torch.empty(P * 2 * gg, 3 * patch * patch, device=x0.device, dtype=cdtype)
+        K = 3 * patch * patch
+        Kp = VitStemFn.kpad(K)
+        patches = torch.empty(P * 2 * gg, Kp, device=x0.device, dtype=cdtype)
         N.vit_im2col(B, Nst, pairs.shape[1], R_, patch, images, pairs, patches)  # recompute
-        _wgrad(dpo, patches, st.g(L.conv_w).view(W, -1))
+        gW = st.g(L.conv_w).view(W, K)  # += dpo^T patches[:, :K]
+        N.gemm(dpo, patches, gW, W, K, dpo.shape[0], trans=1, lda=W, ldb=Kp, accumulate=True)
         st.grad_ready(L.span)
         return None, None, None, None, None, None, None
 

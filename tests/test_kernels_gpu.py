@@ -635,3 +635,25 @@ def test_gemm_wgrad_fused_bias(M, N, K, dtype):
     errb = (outs[0][1].double() - refb).abs().max().item()
     assert errW <= tol * math.sqrt(K) * (1 + refW.abs().max().item()), errW
     assert errb <= tol * math.sqrt(K) * (1 + refb.abs().max().item()), errb
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("R,ps,ld", [(32, 8, 192), (32, 8, 256), (56, 14, 640), (28, 14, 588),
+                                     (64, 32, 3072)])
+def test_vit_im2col_any_patch_padded(dtype, R, ps, ld):
+    """Patch gather for every ViT patch size (ViT-L/14: K = 588 padded to 640 for the GEMM,
+    the pad columns zero)."""
+    B, Nst = 2, 3
+    g = torch.Generator(device="cpu").manual_seed(R + ps + ld)
+    images = torch.randn(B, Nst, 3, R, R, generator=g).to(DEV)
+    pairs = torch.tensor([[[0, 1], [2, 0]], [[1, 2], [2, 1]]], device=DEV)
+    P = B * 2
+    gg = (R // ps) ** 2
+    K = 3 * ps * ps
+    patches = torch.full((P * 2 * gg, ld), 7.0, device=DEV, dtype=dtype)
+    nat.vit_im2col(B, Nst, 2, R, ps, images, pairs, patches)
+    imgs = images[torch.arange(B)[:, None, None].to(DEV), pairs].reshape(P * 2, 3, R, R)
+    ref_p = torch.nn.functional.unfold(imgs, ps, stride=ps).transpose(1, 2).reshape(P * 2 * gg, -1)
+    _close(patches[:, :K], ref_p, dtype)
+    if ld > K:
+        assert float(patches[:, K:].abs().max()) == 0.0
