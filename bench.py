@@ -238,6 +238,44 @@ def bench_config2(batch, steps, warmup, dev):
             "loss": float(loss.item())}
 
 
+def bench_config5(stories, micro, steps, warmup, dev):
+    """BASELINE config 5 shape on one GPU (scripts/recipeqa_finetune.sh): ViT-L/14 (patch 14,
+    1024 wide, 24 layers) + RoBERTa-large-shaped 24 x 1024 joint encoder, N = 9 steps -> 72 pairs
+    per story, 128 tokens per step -> T = 256 + 513 = 769, full training step in bf16 (the
+    reference has no fp8; the fp8 MFMA path is not built)."""
+    preset = model_zoo.PRESETS["config5"]
+    m = model_zoo.build_preset("config5", device=dev, dtype=torch.bfloat16, seed=0)
+    m.train()
+    opt = FusedAdamW(m.stores(), lr=5e-6, warmup=100, total_steps=warmup + steps)
+    data = synthetic_batch(stories, preset["N"], preset["per_seq"], 50265, 224, dev, seed=3000)
+    mbs = [{k: v[o:o + micro] for k, v in data.items()} for o in range(0, stories, micro)]
+    for _ in range(warmup):
+        train_step(m, opt, mbs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = train_step(m, opt, mbs)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    Nst, per = preset["N"], preset["per_seq"]
+    V = m.bert.vision
+    g = 224 // V["patch"]
+    Tv = 1 + 2 * g * g
+    J = preset["joint"]
+    fwd = story_flops(Nst * (Nst - 1), 2 * per, Tv, J["hidden_size"], J["num_hidden_layers"],
+                      V["width"], V["layers"], V["patch"], V["embed"])
+    del m, opt, mbs, data
+    torch.cuda.empty_cache()
+    return {"workload": f"config5 shape: ViT-L/14 + 24x1024 joint encoder + BERSON, N={Nst}, "
+                        f"{Nst * (Nst - 1)} pairs/story, pair seq {2 * per}+{Tv}={2 * per + Tv}, "
+                        f"{stories} stories/step in micro-batches of {micro}, bf16, train mode, 1 GPU",
+            "steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "stories_per_s": stories * steps / dt,
+            "model_tflops": stories * steps / dt * 3 * fwd / 1e12,
+            "model_flops_util": stories * steps / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
+            "fwd_tflop_per_story": fwd / 1e12, "loss": float(loss.item())}
+
+
 def _relaunch(args):
     """`--gpus N` without a torchrun environment: start N ranks under torch.distributed.run as
     a child process (nothing here has touched the GPU) and return its exit code."""
@@ -269,6 +307,7 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=64.0,
                     help="DP all-reduce bucket cap (MB of fp32 grads)")
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 leg")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 leg")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks "
                          "sharing one GPU (RCCL refuses duplicate devices)")
@@ -425,6 +464,11 @@ def main():
             out["config2"] = bench_config2(32, max(3, args.steps), max(1, args.warmup), dev)
         except Exception as e:  # a secondary leg: reported, never required for the headline
             out["config2"] = {"error": repr(e)}
+    if world == 1 and not args.no_config5:
+        try:
+            out["config5"] = bench_config5(2, 1, 2, 1, dev)
+        except Exception as e:
+            out["config5"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config)

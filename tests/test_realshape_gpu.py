@@ -147,6 +147,48 @@ def test_config3_story_bf16_close_to_reference():
 
 
 # ------------------------------------------------------------------------------------------
+# config-5 shape (ViT-L/14 patch 14 -> K 588 padded to 640, width 1024, 16 heads, T = 769,
+# RoBERTa-large width, N = 9 -> 72 pairs) with 2 + 2 layers
+# ------------------------------------------------------------------------------------------
+def _config5_l2(dtype):
+    meta, d = _fixture("real_config5_l2")
+    m = model_zoo.build_from_golden(meta["config"], device=DEV, dtype=dtype)
+    sd = m.state_dict()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                       counter_state_dict({k: tuple(v.shape) for k, v in sd.items()}).items()})
+    m.eval()
+    m.zero_grad()
+    ids, labels, images = real_inputs(meta["input_seed"], meta["config"])
+    inputs = {"input_ids": torch.from_numpy(ids), "labels": torch.from_numpy(labels),
+              "images": torch.from_numpy(images).to(DEV)}
+    return meta, d, m, inputs
+
+
+def test_config5_shape_fp32_matches_reference():
+    meta, d, m, inputs = _config5_l2(torch.float32)
+    loss = m(inputs)[0]
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(d["loss"])) < 1e-4, (loss.item(), float(d["loss"]))
+    grads = {k: p.grad for k, p in m.named_parameters()}
+    gn = sum(float((g.double() ** 2).sum()) for g in grads.values()) ** 0.5
+    assert abs(gn - float(d["grad_norm"])) < 2e-4 * float(d["grad_norm"]), (gn, float(d["grad_norm"]))
+    _check_grads(d, grads)
+    order = berson_pointer_network(m.args, m, None, inputs)
+    assert order == [int(x) for x in d["order"][0]], (order, d["order"])
+
+
+def test_config5_shape_bf16_close_to_reference():
+    meta, d, m, inputs = _config5_l2(torch.bfloat16)
+    loss = m(inputs)[0]
+    loss.backward()
+    torch.cuda.synchronize()
+    ref = float(d["loss"])
+    assert abs(loss.item() - ref) < 2e-2 * abs(ref), (loss.item(), ref)
+    _check_grads(d, {k: p.grad for k, p in m.named_parameters()}, cos_min=0.95)
+
+
+# ------------------------------------------------------------------------------------------
 # single ops at real shape
 # ------------------------------------------------------------------------------------------
 def _store(specs, prefix, dtype):
