@@ -20,15 +20,22 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import kernels as K
+from .checkpoint import JsonConfigMixin, berson_from_pretrained, save_pretrained
 from .params import ParamStore, Spec, attach_tree, linear_specs, ln_specs, normal, uniform, zeros
 from .process_inputs import pairs_generator, prepare_berson_inputs
 
 
-class BersonConfig(SimpleNamespace):
-    """models/berson/configuration_bert.py:77-113 (the fields the head reads)."""
+class BersonConfig(JsonConfigMixin, SimpleNamespace):
+    """models/berson/configuration_bert.py:77-113 (the fields the head reads) plus the
+    PretrainedConfig attributes (configuration_utils.py:46-58) that from_pretrained kwargs may
+    override (train.py:2010-2011 passes num_labels and finetuning_task)."""
 
     def __init__(self, hidden_size=768, num_labels=1, initializer_range=0.02,
                  hidden_dropout_prob=0.1, **kw):
+        for k, v in (("finetuning_task", None), ("output_attentions", False),
+                     ("output_hidden_states", False), ("torchscript", False),
+                     ("use_bfloat16", False), ("pruned_heads", {})):
+            kw.setdefault(k, v)
         super().__init__(hidden_size=hidden_size, num_labels=num_labels,
                          initializer_range=initializer_range,
                          hidden_dropout_prob=hidden_dropout_prob, **kw)
@@ -66,6 +73,10 @@ def _head_specs(H, args, num_labels, std):
 
 
 class BertForOrdering(nn.Module):
+    base_model_prefix = "bert"  # modeling_bert.py:462
+    from_pretrained = classmethod(berson_from_pretrained)  # modeling_utils.py:208-428
+    save_pretrained = save_pretrained  # modeling_utils.py:190-204
+
     def __init__(self, config, args, inner_model=None, tokenizer=None, load_inner_model=False,
                  device="cuda", seed=1, **kw):
         super().__init__()

@@ -17,6 +17,7 @@ import torch
 from torch import nn
 
 from . import kernels as K
+from .checkpoint import JsonConfigMixin, lxrt_from_pretrained, save_pretrained
 from .params import ParamStore, Spec, attach_tree, linear_specs, ln_specs, normal, ones, zeros
 
 VIT = "encoder.visual_model.visual."
@@ -29,7 +30,7 @@ CLIP_VISION = {
 }
 
 
-class LXRTConfig(SimpleNamespace):
+class LXRTConfig(JsonConfigMixin, SimpleNamespace):
     """Subset of lxrt BertConfig (:147-336) that the path reads."""
 
     def __init__(self, vocab_size=50265, hidden_size=768, num_hidden_layers=12,
@@ -115,6 +116,9 @@ def _mark_stale(module, incompatible_keys):
 
 class LXRTModel(nn.Module):
     """VisualBERT-style LXRT encoder over cat(text tokens, CLIP-ViT patch tokens)."""
+
+    from_pretrained = classmethod(lxrt_from_pretrained)  # lxrt:1258-1433 (checkpoint.py)
+    save_pretrained = save_pretrained  # lxrt:1435-1453
 
     def __init__(self, config, multimodal_text_part=False, multimodal_img_part=False, cls_id=0,
                  sep_id=2, max_story_length=5, hl_include_objectives=None, mlm_ignore_index=-100,

@@ -38,6 +38,7 @@ from torch import nn
 
 from . import _native as N
 from . import kernels as K
+from .checkpoint import lxrt_from_pretrained, save_pretrained
 from .lxrt import LXRTConfig, LXRTModel, _mark_stale
 from .params import ParamStore, Spec, attach_tree, linear_specs, ln_specs, normal, zeros
 
@@ -66,6 +67,8 @@ def _pretrain_head_specs(H, vocab, std=0.02, num_answers=2):
 class LXRTPretraining(nn.Module):
     MASK_NUM = 5  # pb_mrm_cls_mask_num (:1694)
     MRM_SCALE = 0.2  # :2347
+    from_pretrained = classmethod(lxrt_from_pretrained)  # roberta/lm_head remaps (checkpoint.py)
+    save_pretrained = save_pretrained
 
     def __init__(self, config, task_mask_lm=True, task_matched=True, task_obj_predict=True,
                  visual_losses="", task_qa=True, num_answers=2, device="cuda",

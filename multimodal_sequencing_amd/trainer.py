@@ -87,6 +87,106 @@ class FusedAdamW:
                 s.refresh_shadows()
         return lr
 
+    # -- checkpoint/resume (trainers/train.py:193-201, 411-413) ---------------------------------
+    def _param_slots(self, model):
+        """[(name, store index, offset, numel)] in model.named_parameters() order (tied
+        parameters once), split into the reference's two groups (train.py:172-183): decay
+        first, then bias / LayerNorm.weight."""
+        where = {}
+        for i, s in enumerate(self.stores):
+            base = s.master.data_ptr()
+            for name, p in s.params.items():
+                where[p.data_ptr()] = (i, (p.data_ptr() - base) // 4, p.numel())
+        from .params import NO_DECAY
+        groups = ([], [])
+        for name, p in model.named_parameters():
+            if p.data_ptr() not in where:
+                raise ValueError(f"parameter {name} is not in the optimizer's stores")
+            i, off, n = where[p.data_ptr()]
+            groups[1 if any(nd in name for nd in NO_DECAY) else 0].append((name, i, off, n))
+        return groups
+
+    def state_dict(self, model):
+        """transformers AdamW.state_dict() layout: {'state': {index: {'step', 'exp_avg',
+        'exp_avg_sq'}}, 'param_groups': [decay group, no-decay group]}, indices running over
+        the groups in model.named_parameters() order. Each group also carries 'param_names'
+        (ignored by torch's loader) so a resume can match by name."""
+        state, groups, idx = {}, [], 0
+        for gi, slots in enumerate(self._param_slots(model)):
+            ids = []
+            for name, i, off, n in slots:
+                shape = model.get_parameter(name).shape
+                if self.step_count > 0:
+                    state[idx] = {"step": self.step_count,
+                                  "exp_avg": self.m[i][off:off + n].view(shape).cpu().clone(),
+                                  "exp_avg_sq": self.v[i][off:off + n].view(shape).cpu().clone()}
+                ids.append(idx)
+                idx += 1
+            groups.append({"lr": self.current_lr(), "betas": tuple(self.betas), "eps": self.eps,
+                           "weight_decay": self.wd if gi == 0 else 0.0, "correct_bias": True,
+                           "initial_lr": self.lr, "params": ids,
+                           "param_names": [s[0] for s in slots]})
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, model, sd):
+        """Restore moments and step from an AdamW state dict written by state_dict() or by the
+        reference's torch.save(optimizer.state_dict()). Parameters are matched by 'param_names'
+        when present, else by position in the reference's group order."""
+        slots = self._param_slots(model)
+        by_name = {s[0]: s for g in slots for s in g}
+        saved = sd["param_groups"]
+        if len(saved) != len(slots):
+            raise ValueError(f"optimizer state has {len(saved)} groups, expected {len(slots)}")
+        steps = set()
+        for gi, g in enumerate(saved):
+            names = g.get("param_names")
+            if names is None:
+                if len(g["params"]) != len(slots[gi]):
+                    raise ValueError(f"group {gi}: {len(g['params'])} params in the state, "
+                                     f"{len(slots[gi])} in the model")
+                targets = slots[gi]
+            else:
+                targets = [by_name[n] for n in names]
+            for pid, (name, i, off, n) in zip(g["params"], targets):
+                st = sd["state"].get(pid, sd["state"].get(str(pid)))
+                if st is None:
+                    continue
+                self.m[i][off:off + n].copy_(st["exp_avg"].reshape(-1).to(self.m[i].device))
+                self.v[i][off:off + n].copy_(st["exp_avg_sq"].reshape(-1).to(self.v[i].device))
+                steps.add(int(st["step"]))
+        if len(steps) > 1:
+            raise ValueError(f"parameters were saved at different steps {sorted(steps)}")
+        self.step_count = steps.pop() if steps else 0
+
+    def scheduler_state_dict(self):
+        """torch LambdaLR.state_dict() of get_linear_schedule_with_warmup after `step_count`
+        scheduler.step() calls (train.py:361-362), for scheduler.pt."""
+        lr = self.current_lr()
+        return {"base_lrs": [self.lr, self.lr], "last_epoch": self.step_count,
+                "_step_count": self.step_count + 1, "verbose": False,
+                "_get_lr_called_within_step": False, "_last_lr": [lr, lr],
+                "lr_lambdas": [None, None]}
+
+    def load_scheduler_state_dict(self, sd):
+        self.step_count = int(sd["last_epoch"])
+
+    def save(self, model, directory):
+        """optimizer.pt + scheduler.pt next to a save_pretrained checkpoint."""
+        from .checkpoint import OPTIMIZER_NAME, SCHEDULER_NAME
+        torch.save(self.state_dict(model), f"{directory}/{OPTIMIZER_NAME}")
+        torch.save(self.scheduler_state_dict(), f"{directory}/{SCHEDULER_NAME}")
+
+    def load(self, model, directory):
+        """train.py:193-201: resume both when both files exist; returns whether it did."""
+        import os
+        from .checkpoint import OPTIMIZER_NAME, SCHEDULER_NAME, load_weights_file
+        o, s = os.path.join(directory, OPTIMIZER_NAME), os.path.join(directory, SCHEDULER_NAME)
+        if not (os.path.isfile(o) and os.path.isfile(s)):
+            return False
+        self.load_state_dict(model, load_weights_file(o))
+        self.load_scheduler_state_dict(load_weights_file(s))
+        return True
+
 
 class GradAllReduce:
     """Data-parallel gradient mean over RCCL (backend "nccl" on ROCm), overlapped with backward.
