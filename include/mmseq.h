@@ -306,6 +306,29 @@ mmseq_status mmseq_span_pool_bwd(int P, int Lt, int H, const void* top, int64_t 
                                  float* dscore, void* dtop, mmseq_dtype dtype,
                                  const mmseq_dropout* drop, mmseq_stream stream);
 
+/* ------------------------------------------------------------------------------------------
+ * BERSON pair expansion on device (process_inputs_for_berson.py:13-368 prepare_berson_inputs,
+ * parse_input_ids :100-110, pairs_generator :246-261, pairwise labels :162-174).
+ *  scan:   per story b (input_ids [B][L], labels [B][N]): steps = the k-th <s> (cls_id) .. k-th
+ *          </s> (sep_id); starts/lens [B][N]; pair j of pairs_generator(N) = (a, c):
+ *          sep_positions[b][j] = (len_a - 1, len_a + len_c - 1), pairwise_labels[b][j] =
+ *          rank[a] < rank[c] with rank = stable argsort(labels[b]); status[0] = max over the
+ *          batch of len_a + len_c (atomicMax: zero it first), status[1] = number of stories
+ *          that do not hold exactly N well-formed steps (the caller raises, as the reference's
+ *          parse does).
+ *  expand: rows r = b*N(N-1) + j of [Lp] (Lp = status[0]): ids = <step a><step c> then pad_id;
+ *          mask = 1 then pad_id (quirk C.7: pads are attended); token type 1 on step c iff
+ *          second_type (cls_id != 0), else 0.
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_pair_scan(int B, int L, int N, const int64_t* input_ids, const int64_t* labels,
+                             int64_t cls_id, int64_t sep_id, int64_t* starts, int64_t* lens,
+                             int64_t* pairwise_labels, int64_t* sep_positions, int32_t* status,
+                             mmseq_stream stream);
+mmseq_status mmseq_pair_expand(int B, int L, int N, int Lp, const int64_t* input_ids,
+                               const int64_t* starts, const int64_t* lens, int64_t pad_id,
+                               int second_type, int64_t* out_ids, int64_t* out_mask,
+                               int64_t* out_token_type, mmseq_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -116,6 +116,9 @@ _SIGS = {
                                                                 ctypes.c_int, _dp, _vp]),
     "mmseq_span_pool_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
                                                                 _vp, ctypes.c_int, _dp, _vp]),
+    "mmseq_pair_scan": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _vp, _c_i64, _c_i64] + [_vp] * 6),
+    "mmseq_pair_expand": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 3 + [_c_i64, ctypes.c_int] +
+                          [_vp] * 4),
 }
 
 EXPORTS = sorted(k for k in _SIGS)
@@ -387,3 +390,33 @@ def span_pool_bwd(P, Lt, H, top, ld_pair, probs, sep, dmix, dscore, dtop, drop=N
     _check(lib().mmseq_span_pool_bwd(P, Lt, H, _p(top), ld_pair, _p(probs), _p(sep), _p(dmix),
                                      _p(dscore), _p(dtop), dt(top), _d(drop), _stream()),
            "mmseq_span_pool_bwd")
+
+
+def pair_scan(input_ids, labels, cls_id, sep_id, starts, lens, plab, sep_pos, status):
+    """status int32 [2], zeroed by the caller: (max pair length, malformed stories)."""
+    B, L = input_ids.shape
+    N = labels.shape[1]
+    for t in (input_ids, labels, starts, lens, plab, sep_pos):
+        if t.dtype != torch.int64 or not t.is_contiguous():
+            raise ValueError("pair_scan: int64 contiguous tensors expected")
+    if tuple(starts.shape) != (B, N) or tuple(lens.shape) != (B, N) or \
+            tuple(plab.shape) != (B, N * (N - 1)) or tuple(sep_pos.shape) != (B, N * (N - 1), 2):
+        raise ValueError("pair_scan: output shapes")
+    if status.dtype != torch.int32 or status.numel() < 2:
+        raise ValueError("pair_scan: status must be int32 [2]")
+    _check(lib().mmseq_pair_scan(B, L, N, _p(input_ids), _p(labels), cls_id, sep_id, _p(starts),
+                                 _p(lens), _p(plab), _p(sep_pos), _p(status), _stream()),
+           "mmseq_pair_scan")
+
+
+def pair_expand(input_ids, starts, lens, N, Lp, pad_id, second_type, out_ids, out_mask, out_tt):
+    B, L = input_ids.shape
+    for t in (out_ids, out_mask, out_tt):
+        if t.dtype != torch.int64 or tuple(t.shape) != (B * N * (N - 1), Lp) or \
+                not t.is_contiguous():
+            raise ValueError("pair_expand: outputs must be int64 [B*N(N-1)][Lp]")
+    if tuple(starts.shape) != (B, N) or tuple(lens.shape) != (B, N):
+        raise ValueError("pair_expand: starts/lens shapes")
+    _check(lib().mmseq_pair_expand(B, L, N, Lp, _p(input_ids), _p(starts), _p(lens), pad_id,
+                                   int(second_type), _p(out_ids), _p(out_mask), _p(out_tt),
+                                   _stream()), "mmseq_pair_expand")
