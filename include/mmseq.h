@@ -329,6 +329,22 @@ mmseq_status mmseq_pair_expand(int B, int L, int N, int Lp, const int64_t* input
                                int second_type, int64_t* out_ids, int64_t* out_mask,
                                int64_t* out_token_type, mmseq_stream stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Image preprocessing (trainers/multimodal_utils.py:195-208, datasets/img_utils.py:27-56,
+ * 135-144: skimage 0.17.2 resize with anti-aliasing + ToTensor + Normalize) for n decoded RGB
+ * uint8 HWC images of any sizes, packed in one buffer:
+ *   table [n][4] int64 on the device = (pixel byte offset, H, W, workspace float offset), the
+ *   workspace offsets a prefix sum of H * 3 * out_w; max_h / max_w bound every H / W;
+ *   out [n][3][out_h][out_w] f32 = (resize(img / 255) - mean[c]) / std[c];
+ *   mean / stdev: 3 host floats each. Workspace: mmseq_image_resize_workspace(heights) bytes.
+ * ------------------------------------------------------------------------------------------ */
+int64_t mmseq_image_resize_workspace(int n_images, const int32_t* heights, int out_w);
+mmseq_status mmseq_image_resize_normalize(int n_images, const uint8_t* pixels,
+                                          const int64_t* table, int max_h, int max_w, int out_h,
+                                          int out_w, const float* mean, const float* stdev,
+                                          float* workspace, int64_t workspace_bytes, float* out,
+                                          mmseq_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

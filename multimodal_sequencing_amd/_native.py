@@ -119,6 +119,9 @@ _SIGS = {
     "mmseq_pair_scan": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _vp, _c_i64, _c_i64] + [_vp] * 6),
     "mmseq_pair_expand": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 3 + [_c_i64, ctypes.c_int] +
                           [_vp] * 4),
+    "mmseq_image_resize_workspace": (ctypes.c_int64, [ctypes.c_int, _vp, ctypes.c_int]),
+    "mmseq_image_resize_normalize": (ctypes.c_int, [ctypes.c_int, _vp, _vp] + [ctypes.c_int] * 4 +
+                                     [_vp, _vp, _vp, _c_i64, _vp, _vp]),
 }
 
 EXPORTS = sorted(k for k in _SIGS)
@@ -420,3 +423,22 @@ def pair_expand(input_ids, starts, lens, N, Lp, pad_id, second_type, out_ids, ou
     _check(lib().mmseq_pair_expand(B, L, N, Lp, _p(input_ids), _p(starts), _p(lens), pad_id,
                                    int(second_type), _p(out_ids), _p(out_mask), _p(out_tt),
                                    _stream()), "mmseq_pair_expand")
+
+
+def image_resize_normalize(pixels, table, heights, max_h, max_w, out, mean, std):
+    """pixels uint8 (device, packed HWC images), table int64 [n][4] (device), heights: host
+    int list (workspace sizing), out f32 [n][3][oh][ow] (device)."""
+    n, _, oh, ow = out.shape
+    if pixels.dtype != torch.uint8 or table.dtype != torch.int64 or tuple(table.shape) != (n, 4):
+        raise ValueError("image_resize: pixels uint8, table int64 [n][4]")
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.shape[1] != 3:
+        raise ValueError("image_resize: out must be contiguous f32 [n][3][oh][ow]")
+    hs = (ctypes.c_int32 * max(n, 1))(*[int(h) for h in heights])
+    wsb = lib().mmseq_image_resize_workspace(n, ctypes.cast(hs, _vp), ow)
+    ws = torch.empty(max(1, wsb // 4), dtype=torch.float32, device=out.device)
+    m = (ctypes.c_float * 3)(*[float(x) for x in mean])
+    s = (ctypes.c_float * 3)(*[float(x) for x in std])
+    _check(lib().mmseq_image_resize_normalize(n, _p(pixels), _p(table), max_h, max_w, oh, ow,
+                                              ctypes.cast(m, _vp), ctypes.cast(s, _vp), _p(ws),
+                                              ws.numel() * 4, _p(out), _stream()),
+           "mmseq_image_resize_normalize")
