@@ -120,6 +120,37 @@ class GemmTimer:
                 "achieved_tflops": f / t / 1e12, "avg_alg_bytes": b / n}
 
 
+def _newest_profile(pattern):
+    import glob
+
+    def order(f):  # r<round>_v<version>: numeric, so v10 sorts after v9
+        m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=order)
+    return files[-1] if files else None
+
+
+def measured_peak():
+    """Dense bf16 MFMA rate measured on MI355X by tools/mfma_peak (random register operands,
+    every SIMD issuing back to back): the best of its two MFMA shapes, or None."""
+    f = _newest_profile("r*_mfma_peak.json")
+    try:
+        d = json.load(open(f))
+        return max(d["bf16_16x16x32_tflops"], d["bf16_32x32x16_tflops"]), os.path.relpath(f, ROOT)
+    except (TypeError, OSError, KeyError, ValueError):
+        return None, None
+
+
+def pmc_mfma_util(group="gemm256_nt"):
+    """MFMA busy fraction of the roofline kernel from the newest committed PMC pass
+    (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 4 SIMD x CUs))."""
+    f = _newest_profile("r*_pmc_mfma_util.json")
+    try:
+        return json.load(open(f))[group]["mfma_util_mean"], os.path.relpath(f, ROOT)
+    except (TypeError, OSError, KeyError, ValueError):
+        return None, None
+
+
 def pmc_traffic(group="gemm256_nt"):
     """Per-launch HBM traffic of the roofline kernel from the newest committed rocprofv3 --pmc
     summary (profiles/r*_pmc_traffic.json, made by tools/pmc_traffic.py: FETCH_SIZE x 2 +
@@ -451,9 +482,16 @@ def main():
         traffic, tsrc = pmc_traffic()
         if (args.config, args.batch, args.micro) != ("config3", 32, 16):
             traffic, tsrc = None, None  # the committed PMC pass profiles the default workload
+        mpeak, msrc = measured_peak()
+        util, usrc = pmc_mfma_util()
+        if (args.config, args.batch, args.micro) != ("config3", 32, 16):
+            util, usrc = None, None
         out["roofline"] = {"bound": "mfma", "kernel": "gemm256_nt_kernel (bf16 NT: fwd + dgrad)",
                            "achieved": gs["achieved_tflops"], "peak": PEAK_BF16_TFLOPS,
                            "unit": "TFLOP/s", "frac": gs["achieved_tflops"] / PEAK_BF16_TFLOPS,
+                           "peak_measured": mpeak, "peak_measured_source": msrc,
+                           "frac_of_measured": (gs["achieved_tflops"] / mpeak) if mpeak else None,
+                           "mfma_busy_pmc": util, "mfma_busy_source": usrc,
                            "traffic": traffic, "traffic_unit": "bytes per launch (PMC)",
                            "traffic_source": tsrc,
                            "algorithmic_bytes_per_launch": gs["avg_alg_bytes"],

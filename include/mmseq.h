@@ -345,6 +345,20 @@ mmseq_status mmseq_image_resize_normalize(int n_images, const uint8_t* pixels,
                                           float* workspace, int64_t workspace_bytes, float* out,
                                           mmseq_stream stream);
 
+/* ------------------------------------------------------------------------------------------
+ * LSTM cell of the pointer decoder (modeling_bert.py:1027-1078, nn.LSTM one step, gates i,f,g,o):
+ *  fwd: gates = gx[b] (row stride ld_gx, x W_ih^T + b_ih, all steps from ONE GEMM) + gh
+ *       (h W_hh^T + b_hh); c_out = f c + i g; h_out = o tanh(c_out); act [B][4H] = (i,f,g,o).
+ *  bwd: dh / dc_next (either may be NULL = zero) -> dgates [B][4H] (pre-activation, shared by the
+ *       x and h GEMMs' backward) and dc_prev.
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_lstm_cell_fwd(int B, int H, const float* gx, int64_t ld_gx, const float* gh,
+                                 const float* c, float* h_out, float* c_out, float* act,
+                                 mmseq_stream stream);
+mmseq_status mmseq_lstm_cell_bwd(int B, int H, const float* act, const float* c,
+                                 const float* c_out, const float* dh, const float* dc_next,
+                                 float* dgates, float* dc_prev, mmseq_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -119,6 +119,8 @@ _SIGS = {
     "mmseq_pair_scan": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _vp, _c_i64, _c_i64] + [_vp] * 6),
     "mmseq_pair_expand": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 3 + [_c_i64, ctypes.c_int] +
                           [_vp] * 4),
+    "mmseq_lstm_cell_fwd": (ctypes.c_int, [ctypes.c_int] * 2 + [_vp, _c_i64] + [_vp] * 6),
+    "mmseq_lstm_cell_bwd": (ctypes.c_int, [ctypes.c_int] * 2 + [_vp] * 8),
     "mmseq_image_resize_workspace": (ctypes.c_int64, [ctypes.c_int, _vp, ctypes.c_int]),
     "mmseq_image_resize_normalize": (ctypes.c_int, [ctypes.c_int, _vp, _vp] + [ctypes.c_int] * 4 +
                                      [_vp, _vp, _vp, _c_i64, _vp, _vp]),
@@ -442,3 +444,23 @@ def image_resize_normalize(pixels, table, heights, max_h, max_w, out, mean, std)
                                               ctypes.cast(m, _vp), ctypes.cast(s, _vp), _p(ws),
                                               ws.numel() * 4, _p(out), _stream()),
            "mmseq_image_resize_normalize")
+
+
+def lstm_cell_fwd(gx, gh, c, h_out, c_out, act):
+    """gx [B][>=4H] rows (stride gx.stride(0)), gh [B][4H], c [B][H] f32."""
+    B, H = c.shape
+    if gx.stride(-1) != 1 or gx.shape[-1] < 4 * H or tuple(gh.shape) != (B, 4 * H):
+        raise ValueError("lstm_cell_fwd: gate shapes")
+    for t in (gx, gh, c, h_out, c_out, act):
+        if t.dtype != torch.float32:
+            raise ValueError("lstm_cell_fwd: f32 tensors expected")
+    _check(lib().mmseq_lstm_cell_fwd(B, H, _p(gx), gx.stride(0), _p(gh), _p(c), _p(h_out),
+                                     _p(c_out), _p(act), _stream()), "mmseq_lstm_cell_fwd")
+
+
+def lstm_cell_bwd(act, c, c_out, dh, dc_next, dgates, dc_prev):
+    B, H = c.shape
+    _check(lib().mmseq_lstm_cell_bwd(B, H, _p(act), _p(c), _p(c_out),
+                                     _p(dh) if dh is not None else None,
+                                     _p(dc_next) if dc_next is not None else None, _p(dgates),
+                                     _p(dc_prev), _stream()), "mmseq_lstm_cell_bwd")

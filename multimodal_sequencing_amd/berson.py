@@ -235,15 +235,17 @@ class BertForOrdering(nn.Module):
             x = f + out
         return self._ln(x, "encoder.layer_norm", 1e-6)
 
-    def _lstm_step(self, x, h, c):
-        """nn.LSTM single step (gate order i, f, g, o)."""
-        g = (K.LinearFn.apply(x, self._anchor, self.store, "decoder.weight_ih_l0",
-                              "decoder.bias_ih_l0", 0)
-             + K.LinearFn.apply(h, self._anchor, self.store, "decoder.weight_hh_l0",
-                                "decoder.bias_hh_l0", 0))
-        i, f, gg, o = g.chunk(4, -1)
-        c2 = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
-        return torch.sigmoid(o) * torch.tanh(c2), c2
+    def _lstm_gx(self, x):
+        """x W_ih^T + b_ih for every decoder input at once (one GEMM, not one per step)."""
+        return K.LinearFn.apply(x, self._anchor, self.store, "decoder.weight_ih_l0",
+                                "decoder.bias_ih_l0", 0)
+
+    def _lstm_step(self, gx, h, c):
+        """nn.LSTM single step (gate order i, f, g, o) from precomputed input gates: the h GEMM
+        and one fused cell kernel (sigmoid/tanh gates, c', h')."""
+        gh = K.LinearFn.apply(h, self._anchor, self.store, "decoder.weight_hh_l0",
+                              "decoder.bias_hh_l0", 0)
+        return K.LstmCellFn.apply(gx, gh, c)
 
     def _forward(self, input_ids, attention_mask=None, token_type_ids=None, pairs_list=None,
                  passage_length=None, pairs_num=None, sep_positions=None, ground_truth=None,
@@ -282,9 +284,10 @@ class BertForOrdering(nn.Module):
         pw_keys = K.LinearFn.apply(pw_info, self._anchor, self.store, "pw_k.weight", None, 0)
         dec_in = torch.cat([doc.new_zeros(B, 1, H), doc[bidx, target[:, :-1]]], 1)  # :998-1002
         h, c = hcn[0][0], hcn[1][0]
+        gx = self._lstm_gx(dec_in)  # [B, N, 4H]
         outs = []
         for t in range(N):
-            h, c = self._lstm_step(dec_in[:, t], h, c)
+            h, c = self._lstm_step(gx[:, t], h, c)
             outs.append(h)
         query = self._lin(torch.stack(outs, 1), "query_linear")
         nll, _logp = K.PointerFn.apply(query, pw_keys, okey, self._anchor, self.store,
@@ -305,7 +308,7 @@ class BertForOrdering(nn.Module):
     def step(self, prev_y, prev_h, prev_c, original_keys, pointed, rela, rela_mask, hist, l1_idx,
              l2_idx):
         """BertForOrdering.step (:1368-1402) for a beam of candidates."""
-        h, c = self._lstm_step(prev_y, prev_h, prev_c)
+        h, c = self._lstm_step(self._lstm_gx(prev_y), prev_h, prev_c)
         q = self._lin(h, "query_linear")[:, None]  # [beam, 1, H]
         nb, T = pointed.shape
         zeros = rela.new_zeros(nb, T, rela.shape[-1])

@@ -327,6 +327,61 @@ __global__ __launch_bounds__(256) void small_attn_bwd_kernel(int B, int T, int h
 
 }  // namespace
 
+
+// ------------------------------------------------------------------------------------------------
+// LSTM cell (modeling_bert.py:1027-1078 nn.LSTM decoder, gate order i, f, g, o), one thread per
+// (row, unit): gates = gx + gh (both already include their biases); saves the four activations.
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void lstm_fwd_kernel(int B, int H, const float* __restrict__ gx,
+                                                       int64_t ldx, const float* __restrict__ gh,
+                                                       const float* __restrict__ c,
+                                                       float* __restrict__ h_out,
+                                                       float* __restrict__ c_out,
+                                                       float* __restrict__ act) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * H) return;
+  const int b = (int)(idx / H), u = (int)(idx - (int64_t)b * H);
+  const float* x = gx + b * ldx;
+  const float* hh = gh + (int64_t)b * 4 * H;
+  const float i = sigm(x[u] + hh[u]);
+  const float f = sigm(x[H + u] + hh[H + u]);
+  const float g = tanhf(x[2 * H + u] + hh[2 * H + u]);
+  const float o = sigm(x[3 * H + u] + hh[3 * H + u]);
+  const float c2 = f * c[idx] + i * g;
+  c_out[idx] = c2;
+  h_out[idx] = o * tanhf(c2);
+  float* a = act + (int64_t)b * 4 * H;
+  a[u] = i;
+  a[H + u] = f;
+  a[2 * H + u] = g;
+  a[3 * H + u] = o;
+}
+
+// dh, dc_next (gradient flowing into c_out) -> dgates (pre-activation) and dc_prev
+__global__ __launch_bounds__(256) void lstm_bwd_kernel(int B, int H, const float* __restrict__ act,
+                                                       const float* __restrict__ c,
+                                                       const float* __restrict__ c_out,
+                                                       const float* __restrict__ dh,
+                                                       const float* __restrict__ dc_next,
+                                                       float* __restrict__ dgates,
+                                                       float* __restrict__ dc_prev) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * H) return;
+  const int b = (int)(idx / H), u = (int)(idx - (int64_t)b * H);
+  const float* a = act + (int64_t)b * 4 * H;
+  const float i = a[u], f = a[H + u], g = a[2 * H + u], o = a[3 * H + u];
+  const float tc = tanhf(c_out[idx]);
+  const float dhv = dh ? dh[idx] : 0.f;
+  const float dc = (dc_next ? dc_next[idx] : 0.f) + dhv * o * (1.f - tc * tc);
+  float* d = dgates + (int64_t)b * 4 * H;
+  d[u] = dc * g * i * (1.f - i);
+  d[H + u] = dc * c[idx] * f * (1.f - f);
+  d[2 * H + u] = dc * i * (1.f - g * g);
+  d[3 * H + u] = dhv * tc * o * (1.f - o);
+  dc_prev[idx] = dc * f;
+}
+
 extern "C" mmseq_status mmseq_pointer_fwd(int B, int N, int H, const float* q, const float* key,
                                           const float* okey, const float* w, const float* w_bias,
                                           const uint8_t* pointed, const int64_t* tgt_len,
@@ -424,4 +479,31 @@ extern "C" mmseq_status mmseq_small_attn_bwd(int B, int T, int heads, int d, con
                      reinterpret_cast<hipStream_t>(stream), B, T, heads, d, q, k, v, probs, dout,
                      scale, dq, dk, dv, make_drop(drop));
   return mmseq_check_launch("small_attn_bwd");
+}
+
+extern "C" mmseq_status mmseq_lstm_cell_fwd(int B, int H, const float* gx, int64_t ld_gx,
+                                            const float* gh, const float* c, float* h_out,
+                                            float* c_out, float* act, mmseq_stream stream) {
+  MMSEQ_REQUIRE(B >= 0 && H > 0 && ld_gx >= 4 * (int64_t)H, "lstm_cell_fwd: bad sizes");
+  MMSEQ_REQUIRE(gx && gh && c && h_out && c_out && act, "lstm_cell_fwd: null buffer");
+  if (B == 0) return MMSEQ_OK;
+  const int64_t n = (int64_t)B * H;
+  hipLaunchKernelGGL(lstm_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, H, gx, ld_gx, gh, c, h_out, c_out,
+                     act);
+  return mmseq_check_launch("lstm_cell_fwd");
+}
+
+extern "C" mmseq_status mmseq_lstm_cell_bwd(int B, int H, const float* act, const float* c,
+                                            const float* c_out, const float* dh,
+                                            const float* dc_next, float* dgates, float* dc_prev,
+                                            mmseq_stream stream) {
+  MMSEQ_REQUIRE(B >= 0 && H > 0, "lstm_cell_bwd: bad sizes");
+  MMSEQ_REQUIRE(act && c && c_out && dgates && dc_prev, "lstm_cell_bwd: null buffer");
+  if (B == 0) return MMSEQ_OK;
+  const int64_t n = (int64_t)B * H;
+  hipLaunchKernelGGL(lstm_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, H, act, c, c_out, dh, dc_next,
+                     dgates, dc_prev);
+  return mmseq_check_launch("lstm_cell_bwd");
 }

@@ -588,6 +588,33 @@ def dropout(x, drop):
     return x if drop is None else DropoutFn.apply(x, drop)
 
 
+class LstmCellFn(torch.autograd.Function):
+    """One nn.LSTM step from precomputed gate inputs: gx = x W_ih^T + b_ih (a row of the one GEMM
+    over all decoder steps) and gh = h W_hh^T + b_hh -> (h', c') (mmseq_lstm_cell_fwd/bwd)."""
+
+    @staticmethod
+    def forward(ctx, gx, gh, c):
+        B, H = c.shape
+        c = c.contiguous()
+        gh = gh.contiguous()
+        if gx.stride(-1) != 1:
+            gx = gx.contiguous()
+        h2, c2 = torch.empty_like(c), torch.empty_like(c)
+        act = torch.empty(B, 4 * H, device=c.device)
+        N.lstm_cell_fwd(gx, gh, c, h2, c2, act)
+        ctx.save_for_backward(act, c, c2)
+        return h2, c2
+
+    @staticmethod
+    def backward(ctx, dh, dc):
+        act, c, c2 = ctx.saved_tensors
+        dg = torch.empty_like(act)
+        dcp = torch.empty_like(c)
+        N.lstm_cell_bwd(act, c, c2, None if dh is None else dh.contiguous(),
+                        None if dc is None else dc.contiguous(), dg, dcp)
+        return dg, dg, dcp
+
+
 class PointerFn(torch.autograd.Function):
     """e = tanh_linear(tanh(q + key + okey)) -> masked log-softmax -> per-step NLL."""
 
