@@ -359,6 +359,27 @@ mmseq_status mmseq_lstm_cell_bwd(int B, int H, const float* act, const float* c,
                                  const float* c_out, const float* dh, const float* dc_next,
                                  float* dgates, float* dc_prev, mmseq_stream stream);
 
+/* ------------------------------------------------------------------------------------------
+ * MX-fp8 forward GEMMs (BASELINE config 5 "fp8 MFMA"; v_mfma_scale_f32_16x16x128_f8f6f4).
+ *  Format: OCP e4m3 elements, one E8M0 scale (2^(s-127)) per 32 consecutive K-elements of a row
+ *  (OCP MX: s = floor(log2 amax) - 8 + 127, elements = x / 2^(s-127) clamped to +-448, RNE).
+ *  Scales are stored "packed": byte ((m/64)*(K/32) + kb)*64 + (m%16)*4 + (m%64)/16, for rows up
+ *  to the next multiple of 64 (mmseq_mxfp8_scale_bytes).
+ *  quant: x [M][K] (bf16 or f32, row stride ldx) -> q [M][K] e4m3 (row stride ldq, % 16 == 0)
+ *         + scales. K % 32 == 0.
+ *  gemm:  C[m][n] bf16 (ldc) = act(alpha * sum_k A[m][k] B[n][k] + bias[n]) + resid[m][n]
+ *         (bias / resid may be NULL; act = mmseq_act); A [M][K], B [N][K] quantised as above,
+ *         K % 128 == 0, lda / ldb % 16 == 0. fp32 accumulation.
+ * ------------------------------------------------------------------------------------------ */
+int64_t mmseq_mxfp8_scale_bytes(int M, int K);
+mmseq_status mmseq_quant_mxfp8(int M, int K, const void* x, int64_t ldx, mmseq_dtype dtype,
+                               void* q, int64_t ldq, void* scales, mmseq_stream stream);
+mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int64_t lda,
+                              const void* a_scales, const void* B, int64_t ldb,
+                              const void* b_scales, void* C, int64_t ldc, const float* bias,
+                              int act, const void* resid, int64_t ldr, float alpha,
+                              mmseq_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

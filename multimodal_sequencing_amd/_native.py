@@ -121,6 +121,12 @@ _SIGS = {
                           [_vp] * 4),
     "mmseq_lstm_cell_fwd": (ctypes.c_int, [ctypes.c_int] * 2 + [_vp, _c_i64] + [_vp] * 6),
     "mmseq_lstm_cell_bwd": (ctypes.c_int, [ctypes.c_int] * 2 + [_vp] * 8),
+    "mmseq_mxfp8_scale_bytes": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
+    "mmseq_quant_mxfp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _c_i64, ctypes.c_int,
+                                         _vp, _c_i64, _vp, _vp]),
+    "mmseq_gemm_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
+                                                            _vp, _c_i64, _vp, ctypes.c_int, _vp,
+                                                            _c_i64, ctypes.c_float, _vp]),
     "mmseq_image_resize_workspace": (ctypes.c_int64, [ctypes.c_int, _vp, ctypes.c_int]),
     "mmseq_image_resize_normalize": (ctypes.c_int, [ctypes.c_int, _vp, _vp] + [ctypes.c_int] * 4 +
                                      [_vp, _vp, _vp, _c_i64, _vp, _vp]),
@@ -464,3 +470,41 @@ def lstm_cell_bwd(act, c, c_out, dh, dc_next, dgates, dc_prev):
                                      _p(dh) if dh is not None else None,
                                      _p(dc_next) if dc_next is not None else None, _p(dgates),
                                      _p(dc_prev), _stream()), "mmseq_lstm_cell_bwd")
+
+
+class MXFP8:
+    """An MX-fp8 operand: q uint8 [rows][K] (OCP e4m3 bits) + packed E8M0 scales."""
+    __slots__ = ("q", "scales", "rows", "K")
+
+    def __init__(self, q, scales, rows, K):
+        self.q, self.scales, self.rows, self.K = q, scales, rows, K
+
+
+def quant_mxfp8(x, out=None):
+    """x [rows][K] bf16 / f32 (K % 32 == 0, unit inner stride) -> MXFP8 (mmseq_quant_mxfp8)."""
+    rows, K = x.shape
+    if x.stride(-1) != 1 or K % 32:
+        raise ValueError("quant_mxfp8: [rows][K] with unit inner stride and K % 32 == 0")
+    ldq = (K + 15) // 16 * 16
+    if out is None:
+        q = torch.empty(rows, ldq, dtype=torch.uint8, device=x.device)
+        sc = torch.empty(lib().mmseq_mxfp8_scale_bytes(rows, K), dtype=torch.uint8,
+                         device=x.device)
+        out = MXFP8(q, sc, rows, K)
+    _check(lib().mmseq_quant_mxfp8(rows, K, _p(x), x.stride(0), dt(x), _p(out.q),
+                                   out.q.stride(0), _p(out.scales), _stream()),
+           "mmseq_quant_mxfp8")
+    return out
+
+
+def gemm_mxfp8(a, b, c, bias=None, act=0, resid=None, alpha=1.0):
+    """c[m][n] (bf16) = act(alpha * a @ b^T + bias) + resid, a / b MXFP8 operands."""
+    if a.K != b.K or tuple(c.shape) != (a.rows, b.rows) or c.dtype != torch.bfloat16:
+        raise ValueError("gemm_mxfp8: shapes / dtype")
+    if resid is not None and (resid.dtype != torch.bfloat16 or tuple(resid.shape) != tuple(c.shape)):
+        raise ValueError("gemm_mxfp8: resid")
+    _check(lib().mmseq_gemm_mxfp8(a.rows, b.rows, a.K, _p(a.q), a.q.stride(0), _p(a.scales),
+                                  _p(b.q), b.q.stride(0), _p(b.scales), _p(c), c.stride(0),
+                                  _p(bias), act, _p(resid),
+                                  resid.stride(0) if resid is not None else 0, alpha, _stream()),
+           "mmseq_gemm_mxfp8")

@@ -1,0 +1,138 @@
+"""MX-fp8 quantiser and GEMM (csrc/fp8.hip) against plain PyTorch references.
+
+* quantiser: bit-exact against a torch restatement of OCP MX quantisation (E8M0 shared exponent
+  floor(log2 amax) - 8 per 32 K-elements, elements x / 2^e clamped to +-448 and rounded to
+  float8_e4m3fn), including all-zero and tiny blocks.
+* GEMM layout / scale selection: operands that quantise exactly (small integers times per-block
+  powers of two) must give the fp64 product to bf16 output rounding.
+* GEMM numerics: against the fp32 product of the dequantised operands (rel. Frobenius <= 5e-3:
+  only the bf16 output rounding and the fp32 summation order differ) and, as the stated fp8
+  tolerance, against the bf16 product of the unquantised operands (rel. Frobenius <= 6e-2).
+* epilogue: bias, GELU (erf) and residual.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def ref_quant(x):
+    """x [rows][K] -> (e4m3 codes uint8 [rows][K], E8M0 bytes [rows][K/32])."""
+    rows, K = x.shape
+    xb = x.float().view(rows, K // 32, 32)
+    amax = xb.abs().amax(-1)
+    e = torch.where(amax > 0, torch.floor(torch.log2(amax)), torch.full_like(amax, -127.0))
+    # floor(log2) from the exponent field, as the kernel (exact for normal floats)
+    bits = amax.view(torch.int32)
+    e = torch.where(amax > 0, ((bits >> 23) & 0xFF).float() - 127, e)
+    e = torch.clamp(e - 8, -127, 127)
+    q = torch.clamp(xb * pow2(-e)[..., None], -448, 448).to(torch.float8_e4m3fn)
+    return q.view(rows, K).view(torch.uint8), (e + 127).to(torch.uint8)
+
+
+def pow2(e):
+    """exact 2^e (float32) for integer-valued e in [-126, 127]; 2^-127 as the subnormal"""
+    e = e.to(torch.int32)
+    normal = ((e + 127).clamp(min=1) << 23).view(torch.float32)
+    return torch.where(e < -126, torch.full_like(normal, 2.0 ** -127), normal)
+
+
+def unpack_scales(packed, rows, K):
+    KB = K // 32
+    m = torch.arange(rows, device=packed.device)
+    kb = torch.arange(KB, device=packed.device)
+    idx = ((m[:, None] // 64) * KB + kb[None]) * 64 + (m[:, None] % 16) * 4 + (m[:, None] % 64) // 16
+    return packed[idx]
+
+
+def dequant(codes, ebytes):
+    rows, K = codes.shape
+    v = codes.view(torch.float8_e4m3fn).float().view(rows, K // 32, 32)
+    return (v * pow2(ebytes.to(torch.int32) - 127)[..., None]).view(rows, K)
+
+
+@pytest.mark.parametrize("rows,K,dtype", [(300, 256, torch.bfloat16), (64, 128, torch.float32),
+                                          (1, 1024, torch.bfloat16)])
+def test_quant_bit_exact(rows, K, dtype):
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows + K)
+    x = torch.randn(rows, K, device=DEV, generator=g)
+    x = x * torch.pow(10.0, torch.randint(-6, 5, (rows, K // 32, 1), device=DEV, generator=g)
+                      .float()).repeat_interleave(32, -1).view(rows, K)
+    x[0, :32] = 0  # an all-zero block -> scale byte 0
+    x = x.to(dtype)
+    mx = N.quant_mxfp8(x)
+    codes, eb = ref_quant(x)
+    got_e = unpack_scales(mx.scales, rows, K)
+    assert torch.equal(got_e, eb)
+    bad = (mx.q[:, :K] != codes).nonzero()
+    if len(bad):
+        r, c = bad[:8, 0], bad[:8, 1]
+        scaled = x.float()[r, c] * pow2(127 - eb[r, c // 32].to(torch.int32))
+        pytest.fail(f"{len(bad)} of {rows * K} codes differ; scaled inputs {scaled.tolist()}, "
+                    f"ours {mx.q[r, c].tolist()}, torch {codes[r, c].tolist()}")
+    assert int(eb[0, 0]) == 0
+    # padded rows of the last 64-row group carry scale 0
+    pad = (64 - rows % 64) % 64
+    if pad:
+        allp = unpack_scales(mx.scales, rows + pad, K)
+        assert int(allp[rows:].max()) == 0
+
+
+def _exact_operand(g, rows, K):
+    v = torch.randint(-7, 8, (rows, K), device=DEV, generator=g).float()
+    e = torch.randint(-4, 5, (rows, K // 32), device=DEV, generator=g).float()
+    return (v.view(rows, K // 32, 32) * torch.pow(2.0, e)[..., None]).view(rows, K)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 256, 512), (1000, 384, 1024)])
+def test_gemm_exact_operands(M, N, K):
+    from multimodal_sequencing_amd import _native as N_
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
+    A = _exact_operand(g, M, K)
+    B = _exact_operand(g, N, K)
+    qa, qb = N_.quant_mxfp8(A), N_.quant_mxfp8(B)
+    assert torch.equal(dequant(qa.q[:, :K], unpack_scales(qa.scales, M, K)), A)  # exact
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    N_.gemm_mxfp8(qa, qb, C)
+    ref = (A.double() @ B.double().T)
+    err = (C.double() - ref).abs() / (ref.abs() + 1.0)
+    assert float(err.max()) < 8e-3, float(err.max())
+
+
+@pytest.mark.parametrize("M,N,K", [(513, 768, 768), (769, 3072, 1024), (1538, 1024, 4096)])
+def test_gemm_random_tolerance(M, N, K):
+    from multimodal_sequencing_amd import _native as N_
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    B = (torch.randn(N, K, device=DEV, generator=g) * 0.02).bfloat16()
+    qa, qb = N_.quant_mxfp8(A), N_.quant_mxfp8(B)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    N_.gemm_mxfp8(qa, qb, C)
+    da = dequant(qa.q[:, :K], unpack_scales(qa.scales, M, K))
+    db = dequant(qb.q[:, :K], unpack_scales(qb.scales, N, K))
+    ref_q = da @ db.T
+    rel_q = float((C.float() - ref_q).norm() / ref_q.norm())
+    assert rel_q < 5e-3, rel_q
+    ref = A.float() @ B.float().T
+    rel = float((C.float() - ref).norm() / ref.norm())
+    assert rel < 6e-2, rel  # the stated MX-fp8 tolerance vs the unquantised product
+
+
+def test_gemm_epilogue_bias_gelu_resid():
+    from multimodal_sequencing_amd import _native as N_
+    g = torch.Generator(device=DEV).manual_seed(3)
+    M, N, K = 300, 256, 256
+    A = _exact_operand(g, M, K) / 64
+    B = _exact_operand(g, N, K) / 64
+    bias = torch.randn(N, device=DEV, generator=g)
+    resid = torch.randn(M, N, device=DEV, generator=g).bfloat16()
+    qa, qb = N_.quant_mxfp8(A), N_.quant_mxfp8(B)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    N_.gemm_mxfp8(qa, qb, C, bias=bias, act=1, resid=resid, alpha=0.5)
+    pre = 0.5 * (A.double() @ B.double().T) + bias.double()
+    ref = torch.nn.functional.gelu(pre) + resid.double()
+    err = (C.double() - ref).abs() / (ref.abs() + 1.0)
+    assert float(err.max()) < 1e-2, float(err.max())
