@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from multimodal_sequencing_amd import _native as N  # noqa: E402
+from multimodal_sequencing_amd import kernels as K  # noqa: E402
 from multimodal_sequencing_amd import model_zoo  # noqa: E402
 from multimodal_sequencing_amd.trainer import (FusedAdamW, GradAllReduce,  # noqa: E402
                                                distributed_indices, train_step)
@@ -272,8 +273,9 @@ def bench_config2(batch, steps, warmup, dev):
 def bench_config5(stories, micro, steps, warmup, dev):
     """BASELINE config 5 shape on one GPU (scripts/recipeqa_finetune.sh): ViT-L/14 (patch 14,
     1024 wide, 24 layers) + RoBERTa-large-shaped 24 x 1024 joint encoder, N = 9 steps -> 72 pairs
-    per story, 128 tokens per step -> T = 256 + 513 = 769, full training step in bf16 (the
-    reference has no fp8; the fp8 MFMA path is not built)."""
+    per story, 128 tokens per step -> T = 256 + 513 = 769, full training step in bf16, plus the
+    eval forward (no grad) in bf16 and with the MX-fp8 encoder GEMMs (kernels.fp8_forward,
+    v_mfma_scale_f32_16x16x128_f8f6f4): stories/s and the fp8 - bf16 loss difference."""
     preset = model_zoo.PRESETS["config5"]
     m = model_zoo.build_preset("config5", device=dev, dtype=torch.bfloat16, seed=0)
     m.train()
@@ -295,6 +297,27 @@ def bench_config5(stories, micro, steps, warmup, dev):
     J = preset["joint"]
     fwd = story_flops(Nst * (Nst - 1), 2 * per, Tv, J["hidden_size"], J["num_hidden_layers"],
                       V["width"], V["layers"], V["patch"], V["embed"])
+    train_loss = float(loss.item())
+    m.eval()
+    fwd_legs = {}
+    with torch.no_grad():
+        for name, fp8 in (("bf16", False), ("mxfp8", True)):
+            with K.fp8_forward(fp8):
+                for _ in range(2):
+                    lv = m(mbs[0])[0]
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    for mb in mbs:
+                        lv = m(mb)[0]
+                torch.cuda.synchronize()
+                fdt = time.perf_counter() - t0
+            fwd_legs[name] = {"stories_per_s": stories * steps / fdt,
+                              "tflops": stories * steps / fdt * fwd / 1e12,
+                              "loss": float(lv.item())}
+    fwd_legs["mxfp8_speedup"] = fwd_legs["mxfp8"]["stories_per_s"] / fwd_legs["bf16"]["stories_per_s"]
+    fwd_legs["mxfp8_loss_rel_diff"] = (abs(fwd_legs["mxfp8"]["loss"] - fwd_legs["bf16"]["loss"]) /
+                                       max(1e-12, abs(fwd_legs["bf16"]["loss"])))
     del m, opt, mbs, data
     torch.cuda.empty_cache()
     return {"workload": f"config5 shape: ViT-L/14 + 24x1024 joint encoder + BERSON, N={Nst}, "
@@ -304,7 +327,8 @@ def bench_config5(stories, micro, steps, warmup, dev):
             "stories_per_s": stories * steps / dt,
             "model_tflops": stories * steps / dt * 3 * fwd / 1e12,
             "model_flops_util": stories * steps / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
-            "fwd_tflop_per_story": fwd / 1e12, "loss": float(loss.item())}
+            "fwd_tflop_per_story": fwd / 1e12, "loss": train_loss,
+            "eval_forward": fwd_legs}
 
 
 def _relaunch(args):

@@ -89,6 +89,7 @@ class ParamStore:
             p.grad = self.grad[o:o + _numel(s.shape)].view(s.shape)
             self.params[s.name] = p
         self.shadow_stale = True
+        self.version = 0  # bumped whenever the compute-dtype weights change (fp8 weight cache)
         # data-parallel hooks (trainer.GradAllReduce): a layer-level autograd Function reports
         # its grad span at the end of its backward (grad_ready) and its start (grad_begin)
         self.grad_hook = None
@@ -164,6 +165,7 @@ class ParamStore:
             src = self.packed(names, "f32")
             N.transpose_cast(src, self.shadow_t[t:t + src.numel()])
         self.shadow_stale = False
+        self.version += 1
 
     # ---------------------------------------------------------------------------------------
     def w(self, name):

@@ -78,6 +78,7 @@ class FusedAdamW:
                     self.betas[1], self.eps, self.wd, self.step_count, self.max_grad_norm, total,
                     shadow)
             # transposed shadows (dgrad operands) from the updated master weights
+            s.version += 1
             if s.compute_dtype == torch.bfloat16:
                 s.shadow_stale = False
                 for first, (t, names) in s.t_offsets.items():

@@ -322,3 +322,19 @@ def test_embeddings_padding_idx(dtype):
         assert np.abs(a[~live]).max(initial=0.0) == 0.0
     assert float(gw[0].abs().max()) == 0.0  # padding_idx 0 row never receives a gradient
     assert float(st.params["position_embeddings.weight"].grad[0].abs().max()) == 0.0
+
+
+def test_config5_shape_fp8_forward_close_to_reference():
+    """MX-fp8 encoder GEMMs (kernels.fp8_forward) in the eval no-grad forward of the config-5
+    shape: loss within 5 % relative of the reference (bf16 alone: 2 %), and the fp8 GEMMs really
+    run (the weight cache fills)."""
+    from multimodal_sequencing_amd import kernels as K
+    meta, d, m, inputs = _config5_l2(torch.bfloat16)
+    with torch.no_grad():
+        base = m(inputs)[0].item()
+        with K.fp8_forward():
+            loss = m(inputs)[0].item()
+            assert len(K._FP8["cache"]) >= 8  # 2 ViT blocks + 2 joint layers x 4 weights
+    ref = float(d["loss"])
+    assert abs(loss - ref) < 5e-2 * abs(ref), (loss, base, ref)
+    assert abs(loss - base) < 5e-2 * abs(ref), (loss, base)
