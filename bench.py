@@ -357,6 +357,8 @@ def main():
     ap.add_argument("--micro", type=int, default=16, help="stories per micro-batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-timer", action="store_true")
+    ap.add_argument("--fwd-micro", type=int, default=0,
+                    help="stories per forward-leg call (0: the whole per-GPU batch)")
     ap.add_argument("--fwd-steps", type=int, default=3,
                     help="forward-only passes timed after the training steps (north-star check)")
     ap.add_argument("--bucket-mb", type=float, default=64.0,
@@ -436,8 +438,12 @@ def main():
     fwd_dt = None
     if args.fwd_steps > 0:
         model.eval()
+        # inference keeps no activations for a backward: the whole per-GPU batch in one pass
+        # (--fwd-micro stories per call), bigger GEMMs and half the launches of the training split
+        fm = max(1, min(args.fwd_micro or args.batch, args.batch))
+        fbs = [{k: v[o:o + fm] for k, v in data.items()} for o in range(0, args.batch, fm)]
         with torch.no_grad():
-            for b in mbs:
+            for b in fbs:
                 model(b)
             torch.cuda.synchronize()
             if world > 1:
@@ -445,7 +451,7 @@ def main():
             torch.cuda.synchronize()
             f0 = time.perf_counter()
             for _ in range(args.fwd_steps):
-                for b in mbs:
+                for b in fbs:
                     model(b)
             torch.cuda.synchronize()
             if world > 1:
@@ -496,9 +502,12 @@ def main():
     }
     if fwd_dt is not None:
         fst = args.batch * args.fwd_steps * world / fwd_dt
+        mpk, _src = measured_peak()
         out["forward"] = {"stories_per_s": fst, "ms_per_batch": fwd_dt / args.fwd_steps * 1e3,
+                          "stories_per_call": fm,
                           "tflops": fst * fwd / 1e12,
                           "mfma_frac": fst * fwd / 1e12 / PEAK_BF16_TFLOPS,
+                          "mfma_frac_of_measured_peak": (fst * fwd / 1e12 / mpk) if mpk else None,
                           "mode": "eval (no dropout), torch.no_grad, full model forward incl. "
                                   "BERSON head + loss; ViT + joint encoder are >99.9% of FLOPs"}
     gs = timer.summary()
