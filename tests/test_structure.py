@@ -70,7 +70,10 @@ def test_code_object_m0_only_feeds_lds_dma():
     so = os.path.join(ROOT, "multimodal_sequencing_amd", "_lib", "libmmseq.so")
     with tempfile.TemporaryDirectory() as d:
         fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
-        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", so], check=True)
+        # explicit output file: objcopy without one rewrites its input in place, which changes
+        # the library under every process that has it mapped (SIGBUS later in this process)
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", so,
+                        os.path.join(d, "copy.so")], check=True)
         subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--type=o", f"--input={fb}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}", "--unbundle"],
                        check=True)
