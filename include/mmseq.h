@@ -380,6 +380,54 @@ mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int64_t lda,
                               int act, const void* resid, int64_t ldr, float alpha,
                               mmseq_stream stream);
 
+/* ------------------------------------------------------------------------------------------
+ * CLIP ModifiedResNet / RN50 (clip/model.py:10-187; lxrt/modeling.py:621-705, 1014-1030), NHWC.
+ *  conv_im2col: x [U][H][W][C] -> cols [U*Ho*Wo][Kp], column (ky*ks + kx)*C + c (zero in the
+ *               padding and past ks*ks*C); the convolution is then the NT GEMM with the weight as
+ *               [Cout][Kp] in the same column order. conv_col2im: the dgrad scatter as a gather.
+ *  bn_fwd:  y = act((x - mean) * rstd * gamma + beta + resid), relu optional; train: batch
+ *           statistics over the rows (Welford partials merged in fixed order), running stats
+ *           updated with momentum and the unbiased variance for n_ref elements; eval: running
+ *           statistics. mean / rstd [C] are written for the backward. Workspace mmseq_bn_workspace.
+ *  bn_bwd:  g = dy * (y > 0 if y != NULL); dgamma += sum g xhat, dbeta += sum g;
+ *           dx = gamma rstd (g - mean g - xhat mean(g xhat)) (train) / gamma rstd g (eval);
+ *           dres = g when non-NULL (the residual branch).
+ *  avgpool2: 2x2 average pool (backward = 1/4 to each input).
+ *  attnpool_gather: pair p's two images (pairimg [P][2], unique image ids) -> x [P][2S+1][C]
+ *           with the reference's reshape-before-permute token order (clip/model.py:77), the mean
+ *           token first and the img_len positional quirk (:79-81); gather_bwd sums the pairs.
+ *  attnpool_out: y [rows][2Ch] = cat(a, a) + visual x/y position + token type (G x G grid);
+ *           out_bwd: da = both halves summed, token_colsum [T2][2Ch] = sum over pairs.
+ * ------------------------------------------------------------------------------------------ */
+mmseq_status mmseq_conv_im2col(int U, int H, int W, int C, int ks, int stride, int pad, int Kp,
+                               const void* x, void* cols, mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_conv_col2im(int U, int H, int W, int C, int ks, int stride, int pad, int Kp,
+                               const void* dcols, void* dx, mmseq_dtype dtype,
+                               mmseq_stream stream);
+int64_t mmseq_bn_workspace(int64_t rows, int C);
+mmseq_status mmseq_bn_fwd(int64_t rows, int C, const void* x, const float* gamma,
+                          const float* beta, const void* resid, int relu, int train, float eps,
+                          float momentum, double n_ref, float* mean, float* rstd,
+                          float* run_mean, float* run_var, void* y, float* workspace,
+                          int64_t workspace_bytes, mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_bn_bwd(int64_t rows, int C, const void* dy, const void* y, const void* x,
+                          const float* mean, const float* rstd, const float* gamma, int train,
+                          float* dgamma, float* dbeta, void* dx, void* dres, float* workspace,
+                          int64_t workspace_bytes, mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_avgpool2(int U, int H, int W, int C, const void* x, void* y, int backward,
+                            mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_attnpool_gather(int P, int S, int C, const void* feats,
+                                   const int32_t* pairimg, const float* pos, void* x,
+                                   mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_attnpool_gather_bwd(int U, int N, int S, int C, int npair, const void* dx,
+                                       const int32_t* rolepairs, void* dfeats,
+                                       mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_attnpool_out(int64_t rows, int T2, int Ch, int G, const void* a,
+                                const float* xpos, const float* ypos, const float* ttype,
+                                void* y, mmseq_dtype dtype, mmseq_stream stream);
+mmseq_status mmseq_attnpool_out_bwd(int P, int T2, int Ch, const void* dy, void* da,
+                                    float* token_colsum, mmseq_dtype dtype, mmseq_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

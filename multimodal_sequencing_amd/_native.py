@@ -127,6 +127,22 @@ _SIGS = {
     "mmseq_gemm_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
                                                             _vp, _c_i64, _vp, ctypes.c_int, _vp,
                                                             _c_i64, ctypes.c_float, _vp]),
+    "mmseq_conv_im2col": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_conv_col2im": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
+    "mmseq_bn_workspace": (ctypes.c_int64, [_c_i64, ctypes.c_int]),
+    "mmseq_bn_fwd": (ctypes.c_int, [_c_i64, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_double,
+                                    _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, ctypes.c_int, _vp]),
+    "mmseq_bn_bwd": (ctypes.c_int, [_c_i64, ctypes.c_int] + [_vp] * 6 + [ctypes.c_int] +
+                     [_vp] * 5 + [_c_i64, ctypes.c_int, _vp]),
+    "mmseq_avgpool2": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp, _vp, ctypes.c_int, ctypes.c_int,
+                                                           _vp]),
+    "mmseq_attnpool_gather": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 4 + [ctypes.c_int, _vp]),
+    "mmseq_attnpool_gather_bwd": (ctypes.c_int, [ctypes.c_int] * 5 + [_vp] * 3 +
+                                  [ctypes.c_int, _vp]),
+    "mmseq_attnpool_out": (ctypes.c_int, [_c_i64] + [ctypes.c_int] * 3 + [_vp] * 5 +
+                           [ctypes.c_int, _vp]),
+    "mmseq_attnpool_out_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 3 + [ctypes.c_int, _vp]),
     "mmseq_image_resize_workspace": (ctypes.c_int64, [ctypes.c_int, _vp, ctypes.c_int]),
     "mmseq_image_resize_normalize": (ctypes.c_int, [ctypes.c_int, _vp, _vp] + [ctypes.c_int] * 4 +
                                      [_vp, _vp, _vp, _c_i64, _vp, _vp]),
@@ -508,3 +524,73 @@ def gemm_mxfp8(a, b, c, bias=None, act=0, resid=None, alpha=1.0):
                                   _p(bias), act, _p(resid),
                                   resid.stride(0) if resid is not None else 0, alpha, _stream()),
            "mmseq_gemm_mxfp8")
+
+
+# -- RN50 (csrc/resnet.hip) ----------------------------------------------------------------------
+def conv_im2col(x, ks, stride, pad, Kp, cols):
+    U, H, W, C = x.shape
+    _check(lib().mmseq_conv_im2col(U, H, W, C, ks, stride, pad, Kp, _p(x), _p(cols), dt(x),
+                                   _stream()), "mmseq_conv_im2col")
+
+
+def conv_col2im(dcols, U, H, W, C, ks, stride, pad, Kp, dx):
+    _check(lib().mmseq_conv_col2im(U, H, W, C, ks, stride, pad, Kp, _p(dcols), _p(dx), dt(dx),
+                                   _stream()), "mmseq_conv_col2im")
+
+
+def _bn_ws(rows, C, device):
+    return torch.empty(max(1, lib().mmseq_bn_workspace(rows, C) // 4), dtype=torch.float32,
+                       device=device)
+
+
+def bn_fwd(x, gamma, beta, resid, relu, train, eps, momentum, n_ref, mean, rstd, run_mean,
+           run_var, y):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    ws = _bn_ws(rows, C, x.device)
+    _check(lib().mmseq_bn_fwd(rows, C, _p(x), _p(gamma), _p(beta), _p(resid), int(relu),
+                              int(train), eps, momentum, float(n_ref), _p(mean), _p(rstd),
+                              _p(run_mean), _p(run_var), _p(y), _p(ws), ws.numel() * 4, dt(x),
+                              _stream()), "mmseq_bn_fwd")
+
+
+def bn_bwd(dy, y, x, mean, rstd, gamma, train, dgamma, dbeta, dx, dres=None):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    ws = _bn_ws(rows, C, x.device)
+    _check(lib().mmseq_bn_bwd(rows, C, _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma),
+                              int(train), _p(dgamma), _p(dbeta), _p(dx), _p(dres), _p(ws),
+                              ws.numel() * 4, dt(x), _stream()), "mmseq_bn_bwd")
+
+
+def avgpool2(x, y, backward=False):
+    """forward: x [U][H][W][C] -> y [U][H/2][W/2][C]; backward: x = dy, y = dx [U][H][W][C]."""
+    U, H, W, C = (y.shape if backward else x.shape)
+    _check(lib().mmseq_avgpool2(U, H, W, C, _p(x), _p(y), int(backward), dt(x), _stream()),
+           "mmseq_avgpool2")
+
+
+def attnpool_gather(feats, pairimg, pos, x):
+    P, T2, C = x.shape
+    S = (T2 - 1) // 2
+    _check(lib().mmseq_attnpool_gather(P, S, C, _p(feats), _p(pairimg), _p(pos), _p(x), dt(x),
+                                       _stream()), "mmseq_attnpool_gather")
+
+
+def attnpool_gather_bwd(dx, N, rolepairs, dfeats):
+    U, S, C = dfeats.shape
+    _check(lib().mmseq_attnpool_gather_bwd(U, N, S, C, N * (N - 1), _p(dx), _p(rolepairs),
+                                           _p(dfeats), dt(dfeats), _stream()),
+           "mmseq_attnpool_gather_bwd")
+
+
+def attnpool_out(a, G, xpos, ypos, ttype, y):
+    rows, Ch = a.shape
+    T2 = 2 * G * G + 1
+    _check(lib().mmseq_attnpool_out(rows, T2, Ch, G, _p(a), _p(xpos), _p(ypos), _p(ttype), _p(y),
+                                    dt(a), _stream()), "mmseq_attnpool_out")
+
+
+def attnpool_out_bwd(dy, P, T2, Ch, da, token_colsum):
+    _check(lib().mmseq_attnpool_out_bwd(P, T2, Ch, _p(dy), _p(da), _p(token_colsum), dt(dy),
+                                        _stream()), "mmseq_attnpool_out_bwd")

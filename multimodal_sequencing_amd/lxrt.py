@@ -18,7 +18,8 @@ from torch import nn
 
 from . import kernels as K
 from .checkpoint import JsonConfigMixin, lxrt_from_pretrained, save_pretrained
-from .params import ParamStore, Spec, attach_tree, linear_specs, ln_specs, normal, ones, zeros
+from .params import (ParamStore, Spec, attach_buffers, attach_tree, linear_specs, ln_specs,
+                     normal, ones, zeros)
 
 VIT = "encoder.visual_model.visual."
 
@@ -27,6 +28,9 @@ CLIP_VISION = {
     "ViT-B/32": dict(width=768, layers=12, patch=32, res=224, embed=512),
     "ViT-B/16": dict(width=768, layers=12, patch=16, res=224, embed=512),
     "ViT-L/14": dict(width=1024, layers=24, patch=14, res=224, embed=768),
+    # ModifiedResNet (clip.py model table: layers (3, 4, 6, 3), width 64, output 1024); the
+    # LXRT visual feature is 2048 wide (param.py:62-64: attnpool output duplicated, :99-101)
+    "RN50": dict(type="rn50", layers=(3, 4, 6, 3), width=64, res=224, embed=1024, feat=2048),
 }
 
 
@@ -57,8 +61,9 @@ def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25, img_part=F
           Spec("embeddings.token_type_embeddings.weight", (cfg.type_vocab_size, H),
                normal(std))]
     sp += ln_specs("embeddings.LayerNorm", H)
+    rn = vision is not None and vision.get("type") == "rn50"
     if not text_part:
-        E = vision["embed"]
+        E = vision.get("feat", vision["embed"])
         sp += linear_specs("encoder.visn_fc.visn_fc", E, H, std=std)
         sp += ln_specs("encoder.visn_fc.visn_layer_norm", H)
         sp += linear_specs("encoder.visn_fc.box_fc", 4, H, std=std, transpose=False)
@@ -78,7 +83,14 @@ def _lxrt_specs(cfg, vision, text_part, max_story_length, pos_num=25, img_part=F
         sp += linear_specs(b + "intermediate.dense", H, I, std=std)
         sp += linear_specs(b + "output.dense", I, H, std=std)
         sp += ln_specs(b + "output.LayerNorm", H)
-    if not text_part:
+    if not text_part and rn:
+        from .resnet import rn50_specs
+        sp += rn50_specs(VIT, vision["layers"], vision["width"], vision["embed"], vision["res"])
+        sp += [Spec("encoder.visual_pos.x_position_embedding.weight", (pos_num, E), normal(std)),
+               Spec("encoder.visual_pos.y_position_embedding.weight", (pos_num, E), normal(std)),
+               Spec("encoder.visual_token_type.token_type_embedding.weight",
+                    (5, E), normal(std))]
+    if not text_part and not rn:
         W, L, p, R, E = (vision[k] for k in ("width", "layers", "patch", "res", "embed"))
         scale = W ** -0.5
         g = R // p
@@ -142,6 +154,21 @@ class LXRTModel(nn.Module):
         self.store.init_weights(seed=kw.get("seed", 0))
         attach_tree(self, self.store.params)
         self._anchor = torch.zeros((), device=device, requires_grad=True)
+        self.rn50 = None
+        if not multimodal_text_part and self.vision.get("type") == "rn50":
+            if multimodal_img_part:
+                raise NotImplementedError("image-only pretraining runs the ViT backbones")
+            from .resnet import RN50Backbone, rn50_buffer_names
+            bufs = {}
+            for name, c in rn50_buffer_names(VIT, self.vision["layers"],
+                                             self.vision["width"]).items():
+                t = (torch.zeros(c, device=device), torch.ones(c, device=device),
+                     torch.zeros((), dtype=torch.long, device=device))
+                attach_buffers(self, {name + ".running_mean": t[0], name + ".running_var": t[1],
+                                      name + ".num_batches_tracked": t[2]})
+                bufs[name] = t
+            self.rn50 = RN50Backbone(self.store, bufs, VIT, "encoder.", self.vision["layers"],
+                                     self.vision["width"])
         self._build_refs()
         self.register_load_state_dict_post_hook(_mark_stale)
         self.dropout_seed = kw.get("seed", 0)  # fold the rank in for data parallel (trainer.py)
@@ -176,7 +203,7 @@ class LXRTModel(nn.Module):
             type=e + "token_type_embeddings.weight", eln_w=e + "LayerNorm.weight",
             eln_b=e + "LayerNorm.bias", v_w=v + "visn_fc.weight", v_b=v + "visn_fc.bias",
             vln_w=v + "visn_layer_norm.weight", vln_b=v + "visn_layer_norm.bias")
-        if not self.text_part:
+        if not self.text_part and self.rn50 is None:
             # the projection lies between the positional embedding and conv1 in the buffer, so the
             # stem's grad span includes it (VitProjFn's backward runs before the stem's)
             self.stem_refs = K.LayerRefs(st, conv_w=VIT + "conv1.weight", cls=VIT + "class_embedding",
@@ -198,7 +225,7 @@ class LXRTModel(nn.Module):
         overlapped data-parallel all-reduce, trainer.GradAllReduce). The ViT projection sits
         inside the stem's span in the buffer, so it is reported with the stem."""
         units = [L.span for L in self.layer_refs] + [self.input_refs.span]
-        if not self.text_part:
+        if not self.text_part and self.rn50 is None:
             units += [L.span for L in self.block_refs]
             units.append(self.stem_refs.span)
         return [u for u in units if u is not None]
@@ -214,6 +241,9 @@ class LXRTModel(nn.Module):
     def visual_forward(self, images, pairs_list):  # CLIP ViT has no dropout (clip/model.py)
         """CLIP ViT over the paired images of every ordered pair (img_len = 2):
         images [B][N][3][R][R] f32 (device), pairs_list [B][npair][2] -> [P*Tv][E]."""
+        if self.rn50 is not None:  # RN50: unique images through the backbone, pairs pooled
+            return self.rn50.forward(images, pairs_list, self._anchor, self.training,
+                                     self.store.compute_dtype)
         st = self.store
         V = self.vision
         W, patch = V["width"], V["patch"]

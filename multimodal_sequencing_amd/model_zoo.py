@@ -19,6 +19,12 @@ PRESETS = {
                                num_attention_heads=12, intermediate_size=3072,
                                max_position_embeddings=514),
                     vision=None, N=5, per_seq=60, ff=3072),
+    # the reference's default backbone (train.py:1011-1019 --clip_model_name RN50, param.py:
+    # 246-247) with the config-3 joint encoder: N=5, 60 tok/step (seq 120 + 99 = 219)
+    "config3_rn50": dict(joint=dict(vocab_size=50265, hidden_size=768, num_hidden_layers=12,
+                                    num_attention_heads=12, intermediate_size=3072,
+                                    max_position_embeddings=514),
+                         vision="RN50", N=5, per_seq=60, ff=3072),
     # config 5: ViT-L/14 + RoBERTa-large shape, N=9, 128 tok/step (seq 256+513=769)
     "config5": dict(joint=dict(vocab_size=50265, hidden_size=1024, num_hidden_layers=24,
                                num_attention_heads=16, intermediate_size=4096,
@@ -44,7 +50,8 @@ def build(joint, vision, N, per_seq, ff=3072, heads=8, inter_layers=2, text_only
         vis = dict(vision) if isinstance(vision, dict) else dict(CLIP_VISION[vision])
     inner = LXRTModel(cfg, multimodal_text_part=text_only, cls_id=0, sep_id=2, max_story_length=N,
                       device=device, compute_dtype=dtype, vision=vis, seed=seed,
-                      clip_model_name=vision if isinstance(vision, str) else "ViT-B/16")
+                      clip_model_name=vision if isinstance(vision, str) else
+                      ("RN50" if vis and vis.get("type") == "rn50" else "ViT-B/16"))
     args = berson_args(N, per_seq, ff=ff, heads=heads, inter_layers=inter_layers,
                        text_only=text_only)
     model = BertForOrdering(BersonConfig(hidden_size=cfg.hidden_size), args, device=device,
@@ -66,8 +73,11 @@ def build_from_golden(cfg, device="cuda", dtype=torch.float32):
     joint = dict(vocab_size=J["vocab"], hidden_size=J["hidden"], num_hidden_layers=J["layers"],
                  num_attention_heads=J["heads"], intermediate_size=J["inter"],
                  max_position_embeddings=J["max_pos"])
-    vision = dict(width=V["width"], layers=V["layers"], patch=V["patch"], res=V["res"],
-                  embed=V["embed"])
+    if V.get("type") == "rn50":
+        vision = dict(V, layers=tuple(V["layers"]))
+    else:
+        vision = dict(width=V["width"], layers=V["layers"], patch=V["patch"], res=V["res"],
+                      embed=V["embed"])
     H = cfg["head"]
     return build(joint, vision, cfg["N"], cfg["per_seq"], ff=H["ff"], heads=H["heads"],
                  inter_layers=H["layers"], text_only=cfg["text_only"], device=device, dtype=dtype)

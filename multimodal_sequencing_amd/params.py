@@ -236,6 +236,19 @@ def attach_tree(root: nn.Module, params):
         mod.register_parameter(parts[-1], p)
 
 
+def attach_buffers(root: nn.Module, buffers):
+    """Register named tensors as module buffers under the dotted names (state_dict entries that
+    are not parameters, e.g. BatchNorm running statistics)."""
+    for name, t in buffers.items():
+        parts = name.split(".")
+        mod = root
+        for part in parts[:-1]:
+            if part not in mod._modules:
+                mod.add_module(part, nn.Module())
+            mod = mod._modules[part]
+        mod.register_buffer(parts[-1], t)
+
+
 def linear_specs(prefix, n_in, n_out, bias=True, std=0.02, transpose=True):
     out = [Spec(prefix + ".weight", (n_out, n_in), normal(std), transpose=transpose)]
     if bias:

@@ -46,6 +46,19 @@ def _scale(key: str, shape) -> tuple:
     if leaf in ("class_embedding", "positional_embedding", "proj"):
         width = shape[0] if leaf == "proj" else shape[-1]
         return (width ** -0.5) / 0.2887, 0.0
+    # ModifiedResNet (RN50): BatchNorm affine / running statistics near identity, convolution
+    # weights with std 1/sqrt(fan_in) so activations keep their scale through 50 layers
+    is_bn = ".bn" in key or "downsample.1." in key
+    if is_bn and leaf == "weight":
+        return 0.4, 1.0
+    if leaf == "running_var":
+        return 0.4, 1.0
+    if leaf == "running_mean":
+        return 0.2, 0.0
+    if leaf == "num_batches_tracked":
+        return 0.0, 0.0
+    if leaf == "weight" and len(shape) == 4 and shape[-1] in (1, 3):
+        return (1.0 / np.sqrt(shape[1] * shape[2] * shape[3])) / 0.2887, 0.0
     if key.startswith("decoder."):  # nn.LSTM default init U(-1/sqrt(H), 1/sqrt(H))
         h = shape[-1] if "weight" in leaf else shape[0] // 4
         return 2.0 / np.sqrt(h), 0.0
