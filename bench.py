@@ -331,6 +331,35 @@ def bench_config5(stories, micro, steps, warmup, dev):
             "eval_forward": fwd_legs}
 
 
+def bench_config3_rn50(stories, micro, steps, warmup, dev):
+    """The reference's default backbone (--clip_model_name RN50, train.py:1011-1019) with the
+    config-3 joint encoder: CLIP ModifiedResNet-50 over each story's 5 images (the product runs the
+    convolutions once per unique image; the reference, once per pair slot: 8x the work), attention
+    pool over each pair's two images (99 tokens), 12 x 768 joint encoder over T = 120 + 99, BERSON,
+    full bf16 training step with train-mode BatchNorm."""
+    m = model_zoo.build_preset("config3_rn50", device=dev, dtype=torch.bfloat16, seed=0)
+    m.train()
+    preset = model_zoo.PRESETS["config3_rn50"]
+    opt = FusedAdamW(m.stores(), lr=5e-6, warmup=100, total_steps=warmup + steps)
+    data = synthetic_batch(stories, preset["N"], preset["per_seq"], 50265, 224, dev, seed=4000)
+    mbs = [{k: v[o:o + micro] for k, v in data.items()} for o in range(0, stories, micro)]
+    for _ in range(warmup):
+        train_step(m, opt, mbs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = train_step(m, opt, mbs)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del m, opt, mbs, data
+    torch.cuda.empty_cache()
+    return {"workload": f"config3_rn50: CLIP RN50 (224^2, unique images) + 12x768 joint encoder + "
+                        f"BERSON, N=5, 20 pairs/story, pair seq 120+99=219, {stories} stories/step "
+                        f"in micro-batches of {micro}, bf16, train mode, 1 GPU",
+            "steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "stories_per_s": stories * steps / dt, "loss": float(loss.item())}
+
+
 def _relaunch(args):
     """`--gpus N` without a torchrun environment: start N ranks under torch.distributed.run as
     a child process (nothing here has touched the GPU) and return its exit code."""
@@ -365,6 +394,7 @@ def main():
                     help="DP all-reduce bucket cap (MB of fp32 grads)")
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 leg")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 leg")
+    ap.add_argument("--no-rn50", action="store_true", help="skip the RN50-backbone leg")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks "
                          "sharing one GPU (RCCL refuses duplicate devices)")
@@ -535,6 +565,11 @@ def main():
             out["config2"] = bench_config2(32, max(3, args.steps), max(1, args.warmup), dev)
         except Exception as e:  # a secondary leg: reported, never required for the headline
             out["config2"] = {"error": repr(e)}
+    if world == 1 and not args.no_rn50:
+        try:
+            out["config3_rn50"] = bench_config3_rn50(32, 16, max(2, args.steps), 1, dev)
+        except Exception as e:  # a secondary leg: reported, never required for the headline
+            out["config3_rn50"] = {"error": repr(e)}
     if world == 1 and not args.no_config5:
         try:
             out["config5"] = bench_config5(2, 1, 2, 1, dev)

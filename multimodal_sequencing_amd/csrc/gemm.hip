@@ -892,7 +892,9 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // the split-K reduction does f32x4 read-modify-writes on C: 16-byte aligned rows only
   const bool c_vec = ((uintptr_t)C & 15) == 0 && ldc % 4 == 0;
-  if (in_dtype == MMSEQ_BF16 && sel.big && bias_grad && c_vec) {
+  // bias-free wgrads (convolution weights) take the same split-K TN kernel, without the fused
+  // column sums
+  if (in_dtype == MMSEQ_BF16 && sel.big && c_vec) {
     GemmArgs t = {};
     t.M = M; t.N = N; t.K = K;
     t.A = A; t.lda = lda; t.B = B; t.ldb = ldb; t.C = C; t.ldc = ldc;
@@ -901,14 +903,15 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
     const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
     int S2 = t256 < g_num_cu ? g_num_cu / t256 : 1;
     if (S2 > K / 1024) S2 = K / 1024 > 0 ? K / 1024 : 1;
-    while (S2 > 1 && (!g_slab || (int64_t)S2 * (M + (int64_t)M * N) * 4 > g_slab_bytes)) --S2;
+    const int64_t cs_rows = bias_grad ? M : 0;
+    while (S2 > 1 && (!g_slab || (int64_t)S2 * (cs_rows + (int64_t)M * N) * 4 > g_slab_bytes)) --S2;
     t.splitk = S2;
     t.kchunk = ((K + S2 - 1) / S2 + 127) / 128 * 128;
     t.splitk = (K + t.kchunk - 1) / t.kchunk;
     if (t.splitk <= 1) { t.splitk = 1; t.kchunk = K; }
     t.slab = g_slab;
     t.cs = bias_grad;
-    t.cs_slab = t.splitk > 1 ? g_slab + (int64_t)t.splitk * M * N : nullptr;
+    t.cs_slab = t.splitk > 1 && bias_grad ? g_slab + (int64_t)t.splitk * M * N : nullptr;
     hipError_t e2 = hipSuccess;
     if (mmseq_gemm256_tn(t, s, &e2)) {
       if (e2 == hipSuccess && t.splitk > 1) {
@@ -916,8 +919,9 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
         const unsigned blocks = (unsigned)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, M, N, t.splitk,
                            g_slab, C, ldc, 1);
-        hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, t.splitk,
-                           t.cs_slab, bias_grad);
+        if (bias_grad)
+          hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, t.splitk,
+                             t.cs_slab, bias_grad);
         e2 = hipGetLastError();
       }
       if (e2 != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_wgrad: %s", hipGetErrorString(e2));

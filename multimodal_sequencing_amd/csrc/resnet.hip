@@ -94,10 +94,12 @@ __global__ __launch_bounds__(256) void col2im_nhwc_kernel(ConvGeom g, const T* _
 }
 
 // ---------------------------------------------------------------------------------------------
-// BatchNorm over rows of [rows][C] (NHWC). Statistics: each block = 64 channels x a chunk of
-// kChunk rows, 4 waves striding the rows; per-thread Welford, Chan-merged across waves, partials
-// (n, mean, M2) per chunk merged in chunk order by the finalize kernel (deterministic).
-constexpr int kChunk = 1024;
+// BatchNorm over rows of [rows][C] (NHWC). Statistics: each block = CPL = min(C, 64) channels x a
+// chunk of kChunk rows; a wave covers 64 / CPL rows per step (C = 32: two rows of 32 channels, so
+// no lane idles), 4 waves stride the chunk; per-thread Welford, Chan-merged across the lanes of a
+// channel and across waves, partials (n, mean, M2) per chunk merged in chunk order by the
+// finalize kernel (deterministic).
+constexpr int kChunk = 4096;
 
 struct Welford {
   float n, mean, m2;
@@ -120,25 +122,29 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(int64_t rows, int C,
                                                                const T* __restrict__ x,
                                                                float* __restrict__ part) {
-  __shared__ float sh[3][4][64];
+  __shared__ float sh[3][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int cpl = C < 64 ? C : 64, rpl = 64 / cpl;
+  const int c = blockIdx.x * cpl + lane % cpl, ro = lane / cpl;
   const int64_t r0 = (int64_t)blockIdx.y * kChunk;
   const int64_t r1 = min(rows, r0 + kChunk);
   Welford s{0.f, 0.f, 0.f};
-  if (c < C)
-    for (int64_t r = r0 + w; r < r1; r += 4) s.push(Elem<T>::ld(x + r * C + c));
-  sh[0][w][lane] = s.n;
-  sh[1][w][lane] = s.mean;
-  sh[2][w][lane] = s.m2;
+  for (int64_t r = r0 + w * rpl + ro; r < r1; r += 4 * rpl) s.push(Elem<T>::ld(x + r * C + c));
+  sh[0][threadIdx.x] = s.n;
+  sh[1][threadIdx.x] = s.mean;
+  sh[2][threadIdx.x] = s.m2;
   __syncthreads();
-  if (w == 0 && c < C) {
-    for (int q = 1; q < 4; ++q) s.merge(sh[0][q][lane], sh[1][q][lane], sh[2][q][lane]);
-    const int64_t o = (int64_t)blockIdx.y * C + c;
+  if (threadIdx.x < cpl) {  // one thread per channel merges its (4 waves x rpl) partials in order
+    Welford t{0.f, 0.f, 0.f};
+    for (int q = 0; q < 4 * rpl; ++q) {
+      const int src = (q / rpl) * 64 + (q % rpl) * cpl + threadIdx.x;
+      t.merge(sh[0][src], sh[1][src], sh[2][src]);
+    }
+    const int64_t o = (int64_t)blockIdx.y * C + blockIdx.x * cpl + threadIdx.x;
     const int64_t nch = gridDim.y;
-    part[o] = s.n;
-    part[nch * C + o] = s.mean;
-    part[2 * nch * C + o] = s.m2;
+    part[o] = t.n;
+    part[nch * C + o] = t.mean;
+    part[2 * nch * C + o] = t.m2;
   }
 }
 
@@ -202,33 +208,35 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(int64_t rows, int C
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ rstd,
                                                              float* __restrict__ part) {
-  __shared__ float sh[2][4][64];
+  __shared__ float sh[2][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int cpl = C < 64 ? C : 64, rpl = 64 / cpl;
+  const int c = blockIdx.x * cpl + lane % cpl, ro = lane / cpl;
   const int64_t r0 = (int64_t)blockIdx.y * kChunk;
   const int64_t r1 = min(rows, r0 + kChunk);
   float sg = 0.f, sgx = 0.f;
-  if (c < C) {
-    const float mu = mean[c], rs = rstd[c];
-    for (int64_t r = r0 + w; r < r1; r += 4) {
-      const int64_t i = r * C + c;
-      float g = Elem<T>::ld(dy + i);
-      if (y && !(Elem<T>::ld(y + i) > 0.f)) g = 0.f;
-      sg += g;
-      sgx += g * (Elem<T>::ld(x + i) - mu) * rs;
-    }
+  const float mu = mean[c], rs = rstd[c];
+  for (int64_t r = r0 + w * rpl + ro; r < r1; r += 4 * rpl) {
+    const int64_t i = r * C + c;
+    float g = Elem<T>::ld(dy + i);
+    if (y && !(Elem<T>::ld(y + i) > 0.f)) g = 0.f;
+    sg += g;
+    sgx += g * (Elem<T>::ld(x + i) - mu) * rs;
   }
-  sh[0][w][lane] = sg;
-  sh[1][w][lane] = sgx;
+  sh[0][threadIdx.x] = sg;
+  sh[1][threadIdx.x] = sgx;
   __syncthreads();
-  if (w == 0 && c < C) {
-    for (int q = 1; q < 4; ++q) {
-      sg += sh[0][q][lane];
-      sgx += sh[1][q][lane];
+  if (threadIdx.x < cpl) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < 4 * rpl; ++q) {
+      const int src = (q / rpl) * 64 + (q % rpl) * cpl + threadIdx.x;
+      a += sh[0][src];
+      b += sh[1][src];
     }
     const int64_t nch = gridDim.y;
-    part[(int64_t)blockIdx.y * C + c] = sg;
-    part[(nch + blockIdx.y) * (int64_t)C + c] = sgx;
+    const int cc = blockIdx.x * cpl + threadIdx.x;
+    part[(int64_t)blockIdx.y * C + cc] = a;
+    part[(nch + blockIdx.y) * (int64_t)C + cc] = b;
   }
 }
 
@@ -489,7 +497,8 @@ extern "C" mmseq_status mmseq_bn_fwd(int64_t rows, int C, const void* x, const f
                                      float* rstd, float* run_mean, float* run_var, void* y,
                                      float* workspace, int64_t workspace_bytes,
                                      mmseq_dtype dtype, mmseq_stream stream) {
-  MMSEQ_REQUIRE(rows >= 0 && C > 0, "bn_fwd: bad sizes");
+  MMSEQ_REQUIRE(rows >= 0 && C > 0 && (C % 64 == 0 || (C <= 64 && 64 % C == 0)),
+                "bn_fwd: C must be a multiple of 64 or divide 64");
   MMSEQ_REQUIRE(x && gamma && beta && mean && rstd && y, "bn_fwd: null buffer");
   MMSEQ_REQUIRE(train || (run_mean && run_var), "bn_fwd: eval needs running statistics");
   if (rows == 0) return MMSEQ_OK;
@@ -498,7 +507,7 @@ extern "C" mmseq_status mmseq_bn_fwd(int64_t rows, int C, const void* x, const f
     MMSEQ_REQUIRE(workspace && workspace_bytes >= mmseq_bn_workspace(rows, C),
                   "bn_fwd: workspace too small");
     const int nch = (int)((rows + kChunk - 1) / kChunk);
-    const dim3 grid((C + 63) / 64, nch);
+    const dim3 grid(C < 64 ? 1 : C / 64, nch);
 #define LAUNCH(T, _) hipLaunchKernelGGL(bn_stats_partial_kernel<T>, grid, dim3(256), 0, s, rows, C, \
                                         (const T*)x, workspace)
     MMSEQ_DT_DISPATCH(dtype, LAUNCH, 0);
@@ -525,14 +534,15 @@ extern "C" mmseq_status mmseq_bn_bwd(int64_t rows, int C, const void* dy, const 
                                      void* dx, void* dres, float* workspace,
                                      int64_t workspace_bytes, mmseq_dtype dtype,
                                      mmseq_stream stream) {
-  MMSEQ_REQUIRE(rows >= 0 && C > 0, "bn_bwd: bad sizes");
+  MMSEQ_REQUIRE(rows >= 0 && C > 0 && (C % 64 == 0 || (C <= 64 && 64 % C == 0)),
+                "bn_bwd: C must be a multiple of 64 or divide 64");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "bn_bwd: null buffer");
   MMSEQ_REQUIRE(workspace_bytes >= mmseq_bn_workspace(rows, C), "bn_bwd: workspace too small");
   if (rows == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int nch = (int)((rows + kChunk - 1) / kChunk);
   float* sums = workspace + 3 * (int64_t)nch * C;
-  const dim3 grid((C + 63) / 64, nch);
+  const dim3 grid(C < 64 ? 1 : C / 64, nch);
 #define LAUNCH(T, _) hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, grid, dim3(256), 0, s, rows, C,   \
                                         (const T*)dy, (const T*)y, (const T*)x, mean, rstd,     \
                                         workspace)

@@ -28,14 +28,10 @@ def _colsum(x, out):
 
 
 def _wgrad(dy, x, gW, gb=None):
-    """gW[out][in] += dy^T x  (dy [R][out], x [R][in]) — TN GEMM accumulating in fp32; with gb the
-    bias gradient gb[out] += sum_r dy[r] is fused into the same pass (mmseq_gemm_wgrad)."""
-    if gb is not None:
-        N.gemm_wgrad(dy, x, gW, gb)
-        return
-    R = dy.numel() // dy.shape[-1]
-    N.gemm(dy, x, gW, gW.shape[0], gW.shape[1], R, trans=1, lda=dy.shape[-1], ldb=x.shape[-1],
-           accumulate=True)
+    """gW[out][in] += dy^T x  (dy [R][out], x [R][in]) — TN GEMM accumulating in fp32 (split-K
+    over R for the bf16 256^2 kernel); with gb the bias gradient gb[out] += sum_r dy[r] is fused
+    into the same pass (mmseq_gemm_wgrad)."""
+    N.gemm_wgrad(dy, x, gW, gb)
 
 
 def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=None, drop=None):
