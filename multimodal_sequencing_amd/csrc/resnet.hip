@@ -33,11 +33,13 @@ struct ConvGeom {
 };
 
 // cols[r][k], r = (u, oy, ox), k = (ky * ks + kx) * C + c; zero past ks*ks*C and in the padding.
-// One thread per 8 columns (C % 8 == 0, Kp % 8 == 0) or per column.
-template <typename T, bool VEC>
+// MODE 1: one thread per 8 columns of one tap (C % 8 == 0, 16-byte load and store); MODE 2: one
+// thread per 8 columns gathered one by one (Kp % 8 == 0: the C = 3 stem), one 16-byte store;
+// MODE 0: one thread per column.
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void im2col_nhwc_kernel(ConvGeom g, const T* __restrict__ x,
                                                           T* __restrict__ cols) {
-  const int per = VEC ? 8 : 1;
+  const int per = MODE ? 8 : 1;
   const int kchunks = g.Kp / per;
   const int64_t rows = (int64_t)g.U * g.Ho * g.Wo;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,13 +49,27 @@ __global__ __launch_bounds__(256) void im2col_nhwc_kernel(ConvGeom g, const T* _
   const int u = (int)(r / (g.Ho * g.Wo));
   const int rem = (int)(r - (int64_t)u * g.Ho * g.Wo);
   const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+  T* dst = cols + r * g.Kp + k;
+  if constexpr (MODE == 2) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = k + j, tap = kk / g.C, c = kk - tap * g.C;
+      const int ky = tap / g.ks, kx = tap - ky * g.ks;
+      const int iy = oy * g.stride + ky - g.pad, ix = ox * g.stride + kx - g.pad;
+      const bool in = tap < g.ks * g.ks && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+      v[j] = in ? Elem<T>::ld(x + (((int64_t)u * g.H + iy) * g.W + ix) * g.C + c) : 0.f;
+    }
+    Vec4<T>::st(dst, (f32x4){v[0], v[1], v[2], v[3]});
+    Vec4<T>::st(dst + 4, (f32x4){v[4], v[5], v[6], v[7]});
+    return;
+  }
   const int tap = k / g.C, c = k - tap * g.C;
   const int ky = tap / g.ks, kx = tap - ky * g.ks;
   const int iy = oy * g.stride + ky - g.pad, ix = ox * g.stride + kx - g.pad;
   const bool in = tap < g.ks * g.ks && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
   const T* src = x + (((int64_t)u * g.H + iy) * g.W + ix) * g.C + c;
-  T* dst = cols + r * g.Kp + k;
-  if constexpr (VEC) {
+  if constexpr (MODE == 1) {
     Pack8<T> p;
     if (in) p.ld(src); else p.zero();
     p.st(dst);
@@ -62,20 +78,24 @@ __global__ __launch_bounds__(256) void im2col_nhwc_kernel(ConvGeom g, const T* _
   }
 }
 
-// dx[u][iy][ix][c] = sum over taps of dcols at the output positions that read (iy, ix)
-template <typename T>
+// dx[u][iy][ix][c] = sum over taps of dcols at the output positions that read (iy, ix); PER
+// channels per thread (8 with 16-byte accesses when C % 8 == 0)
+template <typename T, int PER>
 __global__ __launch_bounds__(256) void col2im_nhwc_kernel(ConvGeom g, const T* __restrict__ dcols,
                                                           T* __restrict__ dx) {
-  const int64_t total = (int64_t)g.U * g.H * g.W * g.C;
+  const int cg = g.C / PER;
+  const int64_t total = (int64_t)g.U * g.H * g.W * cg;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int c = (int)(idx % g.C);
-  int64_t t = idx / g.C;
+  const int c = (int)(idx % cg) * PER;
+  int64_t t = idx / cg;
   const int ix = (int)(t % g.W);
   t /= g.W;
   const int iy = (int)(t % g.H);
   const int u = (int)(t / g.H);
-  float acc = 0.f;
+  float acc[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) acc[j] = 0.f;
   for (int ky = 0; ky < g.ks; ++ky) {
     const int yy = iy + g.pad - ky;
     if (yy < 0 || yy % g.stride) continue;
@@ -87,28 +107,123 @@ __global__ __launch_bounds__(256) void col2im_nhwc_kernel(ConvGeom g, const T* _
       const int ox = xx / g.stride;
       if (ox >= g.Wo) continue;
       const int64_t r = ((int64_t)u * g.Ho + oy) * g.Wo + ox;
-      acc += Elem<T>::ld(dcols + r * g.Kp + (ky * g.ks + kx) * g.C + c);
+      const T* src = dcols + r * g.Kp + (ky * g.ks + kx) * g.C + c;
+      if constexpr (PER == 8) {
+        const f32x4 a = Vec4<T>::ld(src), b = Vec4<T>::ld(src + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j] += a[j];
+          acc[4 + j] += b[j];
+        }
+      } else {
+        acc[0] += Elem<T>::ld(src);
+      }
     }
   }
-  Elem<T>::st(dx + idx, acc);
+  T* dst = dx + (((int64_t)u * g.H + iy) * g.W + ix) * g.C + c;
+  if constexpr (PER == 8) {
+    Vec4<T>::st(dst, (f32x4){acc[0], acc[1], acc[2], acc[3]});
+    Vec4<T>::st(dst + 4, (f32x4){acc[4], acc[5], acc[6], acc[7]});
+  } else {
+    Elem<T>::st(dst, acc[0]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
-// BatchNorm over rows of [rows][C] (NHWC). Statistics: each block = CPL = min(C, 64) channels x a
-// chunk of kChunk rows; a wave covers 64 / CPL rows per step (C = 32: two rows of 32 channels, so
-// no lane idles), 4 waves stride the chunk; per-thread Welford, Chan-merged across the lanes of a
-// channel and across waves, partials (n, mean, M2) per chunk merged in chunk order by the
-// finalize kernel (deterministic).
-constexpr int kChunk = 4096;
+// BatchNorm over rows of [rows][C] (NHWC), HBM-bound: every thread moves 8 consecutive channels
+// (16 B of bf16). A statistics block covers CW = min(C, 512) channels (CW / 8 lanes per row,
+// 2048 / CW rows per block step) over a chunk of rows; the chunk length is chosen so the grid has
+// ~1024 blocks. Per-thread sums are shifted by the chunk's first row (sum d, sum d^2 with
+// d = x - x[r0]), added across the block in a fixed order, and turned into per-chunk partials
+// (n, mean, M2) that the finalize kernel Chan-merges in chunk order: deterministic.
+struct BnPlan {
+  int cw, lpr, rpb, gx;  // channels per block, lanes per row, rows per block step, channel blocks
+  int64_t chunk;         // rows per chunk (multiple of rpb)
+  int nch;               // chunks
+};
+
+__host__ inline bool bn_shape_ok(int C) {
+  return C % 8 == 0 && (C > 512 ? C % 512 == 0 : (256 % (C / 8)) == 0);
+}
+
+__host__ inline BnPlan bn_plan(int64_t rows, int C) {
+  BnPlan p;
+  p.cw = C < 512 ? C : 512;
+  p.lpr = p.cw / 8;
+  p.rpb = 256 / p.lpr;
+  p.gx = C / p.cw;
+  const int64_t want = (rows * p.gx + 1023) / 1024;  // rows per chunk for ~1024 blocks
+  int64_t ch = want < 4 * p.rpb ? 4 * p.rpb : want;
+  p.chunk = (ch + p.rpb - 1) / p.rpb * p.rpb;
+  p.nch = rows > 0 ? (int)((rows + p.chunk - 1) / p.chunk) : 0;
+  return p;
+}
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float* v) {
+  const f32x4 a = Vec4<T>::ld(p), b = Vec4<T>::ld(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = a[j];
+    v[4 + j] = b[j];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float* v) {
+  Vec4<T>::st(p, (f32x4){v[0], v[1], v[2], v[3]});
+  Vec4<T>::st(p + 4, (f32x4){v[4], v[5], v[6], v[7]});
+}
+__device__ __forceinline__ void ldf8(const float* p, float* v) { ld8<float>(p, v); }
+
+// per-chunk partials part[k][C] (n), part[nch + k][C] (mean), part[2 nch + k][C] (M2)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int64_t rows, int C, BnPlan pl,
+                                                               const T* __restrict__ x,
+                                                               float* __restrict__ part) {
+  __shared__ float sh[2][2048];
+  const int lp = threadIdx.x % pl.lpr, rr = threadIdx.x / pl.lpr;
+  const int c0 = blockIdx.x * pl.cw + lp * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * pl.chunk;
+  const int64_t r1 = min(rows, r0 + pl.chunk);
+  float k[8], s[8], q[8];
+  ld8(x + r0 * C + c0, k);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+#pragma unroll 2
+  for (int64_t r = r0 + rr; r < r1; r += pl.rpb) {
+    float v[8];
+    ld8(x + r * C + c0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = v[j] - k[j];
+      s[j] += d;
+      q[j] = fmaf(d, d, q[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][rr * pl.cw + lp * 8 + j] = s[j];
+    sh[1][rr * pl.cw + lp * 8 + j] = q[j];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < pl.cw; t += 256) {
+    float S = 0.f, Q = 0.f;
+    for (int i = 0; i < pl.rpb; ++i) {
+      S += sh[0][i * pl.cw + t];
+      Q += sh[1][i * pl.cw + t];
+    }
+    const int c = blockIdx.x * pl.cw + t;
+    const float n = (float)(r1 - r0), kk = Elem<T>::ld(x + r0 * C + c);
+    const float m = S / n;
+    const int64_t o = (int64_t)blockIdx.y * C + c, stride = (int64_t)pl.nch * C;
+    part[o] = n;
+    part[stride + o] = kk + m;
+    part[2 * stride + o] = fmaxf(Q - S * m, 0.f);
+  }
+}
 
 struct Welford {
   float n, mean, m2;
-  __device__ __forceinline__ void push(float x) {
-    n += 1.f;
-    const float d = x - mean;
-    mean += d / n;
-    m2 += d * (x - mean);
-  }
   __device__ __forceinline__ void merge(float nb, float mb, float m2b) {
     if (nb == 0.f) return;
     const float nn = n + nb, d = mb - mean;
@@ -118,56 +233,36 @@ struct Welford {
   }
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int64_t rows, int C,
-                                                               const T* __restrict__ x,
-                                                               float* __restrict__ part) {
-  __shared__ float sh[3][256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int cpl = C < 64 ? C : 64, rpl = 64 / cpl;
-  const int c = blockIdx.x * cpl + lane % cpl, ro = lane / cpl;
-  const int64_t r0 = (int64_t)blockIdx.y * kChunk;
-  const int64_t r1 = min(rows, r0 + kChunk);
-  Welford s{0.f, 0.f, 0.f};
-  for (int64_t r = r0 + w * rpl + ro; r < r1; r += 4 * rpl) s.push(Elem<T>::ld(x + r * C + c));
-  sh[0][threadIdx.x] = s.n;
-  sh[1][threadIdx.x] = s.mean;
-  sh[2][threadIdx.x] = s.m2;
-  __syncthreads();
-  if (threadIdx.x < cpl) {  // one thread per channel merges its (4 waves x rpl) partials in order
-    Welford t{0.f, 0.f, 0.f};
-    for (int q = 0; q < 4 * rpl; ++q) {
-      const int src = (q / rpl) * 64 + (q % rpl) * cpl + threadIdx.x;
-      t.merge(sh[0][src], sh[1][src], sh[2][src]);
-    }
-    const int64_t o = (int64_t)blockIdx.y * C + blockIdx.x * cpl + threadIdx.x;
-    const int64_t nch = gridDim.y;
-    part[o] = t.n;
-    part[nch * C + o] = t.mean;
-    part[2 * nch * C + o] = t.m2;
-  }
-}
-
 // mean / rstd from the partials; train-mode running-stat update (momentum, unbiased variance with
 // the reference's element count n_ref, which counts each image as often as the reference's
-// batch holds it)
-__global__ __launch_bounds__(256) void bn_stats_final_kernel(int C, int nch, const float* part,
-                                                             float eps, float momentum,
-                                                             double n_ref, float* mean,
-                                                             float* rstd, float* run_mean,
-                                                             float* run_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// batch holds it). Block = 32 channels x 32 chunk lanes: lane j merges chunks j, j + 32, ... in
+// order, then lane 0 merges the 32 lane results in order (deterministic).
+__global__ __launch_bounds__(1024) void bn_stats_final_kernel(int C, int nch, const float* part,
+                                                              float eps, float momentum,
+                                                              double n_ref, float* mean,
+                                                              float* rstd, float* run_mean,
+                                                              float* run_var) {
+  __shared__ float sh[3][32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + tx;
   Welford s{0.f, 0.f, 0.f};
-  for (int k = 0; k < nch; ++k)
-    s.merge(part[(int64_t)k * C + c], part[((int64_t)nch + k) * C + c],
-            part[(2 * (int64_t)nch + k) * C + c]);
-  const float var = s.n > 0.f ? s.m2 / s.n : 0.f;
-  mean[c] = s.mean;
+  if (c < C)
+    for (int k = ty; k < nch; k += 32)
+      s.merge(part[(int64_t)k * C + c], part[((int64_t)nch + k) * C + c],
+              part[(2 * (int64_t)nch + k) * C + c]);
+  sh[0][ty][tx] = s.n;
+  sh[1][ty][tx] = s.mean;
+  sh[2][ty][tx] = s.m2;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  Welford t{0.f, 0.f, 0.f};
+  for (int j = 0; j < 32; ++j) t.merge(sh[0][j][tx], sh[1][j][tx], sh[2][j][tx]);
+  const float var = t.n > 0.f ? t.m2 / t.n : 0.f;
+  mean[c] = t.mean;
   rstd[c] = rsqrtf(var + eps);
   if (run_mean) {
     const double unb = n_ref > 1.0 ? (double)var * n_ref / (n_ref - 1.0) : (double)var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * s.mean;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * t.mean;
     run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
   }
 }
@@ -181,9 +276,9 @@ __global__ __launch_bounds__(256) void bn_eval_stats_kernel(int C, float eps, co
   rstd[c] = rsqrtf(run_var[c] + eps);
 }
 
-// y = act((x - mean) * rstd * gamma + beta + resid)
+// y = act((x - mean) * rstd * gamma + beta + resid), 8 channels per thread
 template <typename T>
-__global__ __launch_bounds__(256) void bn_apply_kernel(int64_t n, int C, const T* __restrict__ x,
+__global__ __launch_bounds__(256) void bn_apply_kernel(int64_t n8, int C, const T* __restrict__ x,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
                                                        const float* __restrict__ gamma,
@@ -191,75 +286,112 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t n, int C, const T
                                                        const T* __restrict__ resid, int relu,
                                                        T* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int c = (int)(i % C);
-  float v = (Elem<T>::ld(x + i) - mean[c]) * rstd[c] * gamma[c] + beta[c];
-  if (resid) v += Elem<T>::ld(resid + i);
-  if (relu) v = fmaxf(v, 0.f);
-  Elem<T>::st(y + i, v);
+  if (i >= n8) return;
+  const int64_t e = i * 8;
+  const int c = (int)(e % C);
+  float v[8], mu[8], rs[8], ga[8], be[8];
+  ld8(x + e, v);
+  ldf8(mean + c, mu);
+  ldf8(rstd + c, rs);
+  ldf8(gamma + c, ga);
+  ldf8(beta + c, be);
+  float r[8];
+  if (resid) ld8(resid + e, r);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = fmaf((v[j] - mu[j]) * rs[j], ga[j], be[j]);
+    if (resid) t += r[j];
+    v[j] = relu ? fmaxf(t, 0.f) : t;
+  }
+  st8(y + e, v);
 }
 
-// backward partial sums per chunk: sum g, sum g * xhat with g = dy * (y > 0 when relu)
+// backward partial sums per chunk: sum g, sum g * xhat with g = dy * (y > 0 when relu);
+// part[k][C] = sum g, part[nch + k][C] = sum g xhat
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(int64_t rows, int C,
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(int64_t rows, int C, BnPlan pl,
                                                              const T* __restrict__ dy,
                                                              const T* __restrict__ y,
                                                              const T* __restrict__ x,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ rstd,
                                                              float* __restrict__ part) {
-  __shared__ float sh[2][256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int cpl = C < 64 ? C : 64, rpl = 64 / cpl;
-  const int c = blockIdx.x * cpl + lane % cpl, ro = lane / cpl;
-  const int64_t r0 = (int64_t)blockIdx.y * kChunk;
-  const int64_t r1 = min(rows, r0 + kChunk);
-  float sg = 0.f, sgx = 0.f;
-  const float mu = mean[c], rs = rstd[c];
-  for (int64_t r = r0 + w * rpl + ro; r < r1; r += 4 * rpl) {
-    const int64_t i = r * C + c;
-    float g = Elem<T>::ld(dy + i);
-    if (y && !(Elem<T>::ld(y + i) > 0.f)) g = 0.f;
-    sg += g;
-    sgx += g * (Elem<T>::ld(x + i) - mu) * rs;
-  }
-  sh[0][threadIdx.x] = sg;
-  sh[1][threadIdx.x] = sgx;
-  __syncthreads();
-  if (threadIdx.x < cpl) {
-    float a = 0.f, b = 0.f;
-    for (int q = 0; q < 4 * rpl; ++q) {
-      const int src = (q / rpl) * 64 + (q % rpl) * cpl + threadIdx.x;
-      a += sh[0][src];
-      b += sh[1][src];
+  __shared__ float sh[2][2048];
+  const int lp = threadIdx.x % pl.lpr, rr = threadIdx.x / pl.lpr;
+  const int c0 = blockIdx.x * pl.cw + lp * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * pl.chunk;
+  const int64_t r1 = min(rows, r0 + pl.chunk);
+  float mu[8], rs[8], sg[8], sgx[8];
+  ldf8(mean + c0, mu);
+  ldf8(rstd + c0, rs);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+#pragma unroll 2
+  for (int64_t r = r0 + rr; r < r1; r += pl.rpb) {
+    float g[8], xv[8];
+    ld8(dy + r * C + c0, g);
+    ld8(x + r * C + c0, xv);
+    if (y) {
+      float yv[8];
+      ld8(y + r * C + c0, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
     }
-    const int64_t nch = gridDim.y;
-    const int cc = blockIdx.x * cpl + threadIdx.x;
-    part[(int64_t)blockIdx.y * C + cc] = a;
-    part[(nch + blockIdx.y) * (int64_t)C + cc] = b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sg[j] += g[j];
+      sgx[j] = fmaf(g[j], (xv[j] - mu[j]) * rs[j], sgx[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][rr * pl.cw + lp * 8 + j] = sg[j];
+    sh[1][rr * pl.cw + lp * 8 + j] = sgx[j];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < pl.cw; t += 256) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < pl.rpb; ++i) {
+      a += sh[0][i * pl.cw + t];
+      b += sh[1][i * pl.cw + t];
+    }
+    const int c = blockIdx.x * pl.cw + t;
+    part[(int64_t)blockIdx.y * C + c] = a;
+    part[((int64_t)pl.nch + blockIdx.y) * C + c] = b;
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_final_kernel(int C, int nch, const float* part,
-                                                           float* sums, float* dgamma,
-                                                           float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int C, int nch, const float* part,
+                                                            float* sums, float* dgamma,
+                                                            float* dbeta) {
+  __shared__ float sh[2][32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + tx;
   float sg = 0.f, sgx = 0.f;
-  for (int k = 0; k < nch; ++k) {
-    sg += part[(int64_t)k * C + c];
-    sgx += part[((int64_t)nch + k) * C + c];
+  if (c < C)
+    for (int k = ty; k < nch; k += 32) {
+      sg += part[(int64_t)k * C + c];
+      sgx += part[((int64_t)nch + k) * C + c];
+    }
+  sh[0][ty][tx] = sg;
+  sh[1][ty][tx] = sgx;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int j = 0; j < 32; ++j) {
+    a += sh[0][j][tx];
+    b += sh[1][j][tx];
   }
-  sums[c] = sg;
-  sums[C + c] = sgx;
-  if (dgamma) dgamma[c] += sgx;
-  if (dbeta) dbeta[c] += sg;
+  sums[c] = a;
+  sums[C + c] = b;
+  if (dgamma) dgamma[c] += b;
+  if (dbeta) dbeta[c] += a;
 }
 
 // dx = gamma rstd (g - sum g / n - xhat sum(g xhat) / n)  (train; eval: gamma rstd g);
-// dres = g (the residual branch's gradient) when requested
+// dres = g (the residual branch's gradient) when requested; 8 channels per thread
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t n, int C, int64_t rows,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t n8, int C, int64_t rows,
                                                            const T* __restrict__ dy,
                                                            const T* __restrict__ y,
                                                            const T* __restrict__ x,
@@ -270,19 +402,38 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t n, int C, int
                                                            int train, T* __restrict__ dx,
                                                            T* __restrict__ dres) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int c = (int)(i % C);
-  float g = Elem<T>::ld(dy + i);
-  if (y && !(Elem<T>::ld(y + i) > 0.f)) g = 0.f;
-  if (dres) Elem<T>::st(dres + i, g);
-  const float rs = rstd[c];
-  float v = g;
+  if (i >= n8) return;
+  const int64_t e = i * 8;
+  const int c = (int)(e % C);
+  float g[8], rs[8], ga[8];
+  ld8(dy + e, g);
+  if (y) {
+    float yv[8];
+    ld8(y + e, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+  }
+  if (dres) st8(dres + e, g);
+  ldf8(rstd + c, rs);
+  ldf8(gamma + c, ga);
+  float v[8];
   if (train) {
     const float inv = 1.f / (float)rows;
-    const float xh = (Elem<T>::ld(x + i) - mean[c]) * rs;
-    v = g - sums[c] * inv - xh * sums[C + c] * inv;
+    float xv[8], mu[8], s1[8], s2[8];
+    ld8(x + e, xv);
+    ldf8(mean + c, mu);
+    ldf8(sums + c, s1);
+    ldf8(sums + C + c, s2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xv[j] - mu[j]) * rs[j];
+      v[j] = (g[j] - s1[j] * inv - xh * s2[j] * inv) * rs[j] * ga[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = g[j] * rs[j] * ga[j];
   }
-  Elem<T>::st(dx + i, v * rs * gamma[c]);
+  st8(dx + e, v);
 }
 
 // 2x2 average pool, NHWC
@@ -459,12 +610,15 @@ extern "C" mmseq_status mmseq_conv_im2col(int U, int H, int W, int C, int ks, in
              stride, pad, Kp};
   const int64_t rows = (int64_t)U * g.Ho * g.Wo;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool vec = C % 8 == 0 && Kp % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)cols & 15) == 0;
-#define LAUNCH(T, V)                                                                       \
-  hipLaunchKernelGGL((im2col_nhwc_kernel<T, V>), dim3(blocks<T>(rows * (Kp / (V ? 8 : 1)))), \
-                     dim3(256), 0, s, g, (const T*)x, (T*)cols)
-  if (dtype == MMSEQ_BF16) { if (vec) LAUNCH(unsigned short, true); else LAUNCH(unsigned short, false); }
-  else { if (vec) LAUNCH(float, true); else LAUNCH(float, false); }
+  const bool al = ((uintptr_t)cols & 15) == 0 && Kp % 8 == 0;
+  const int mode = al && C % 8 == 0 && ((uintptr_t)x & 15) == 0 ? 1 : al ? 2 : 0;
+  const dim3 grid((unsigned)((rows * (Kp / (mode ? 8 : 1)) + 255) / 256));
+#define LAUNCH(T, M) hipLaunchKernelGGL((im2col_nhwc_kernel<T, M>), grid, dim3(256), 0, s, g, \
+                                        (const T*)x, (T*)cols)
+#define LAUNCH3(T, _) \
+  if (mode == 1) LAUNCH(T, 1); else if (mode == 2) LAUNCH(T, 2); else LAUNCH(T, 0)
+  MMSEQ_DT_DISPATCH(dtype, LAUNCH3, 0);
+#undef LAUNCH3
 #undef LAUNCH
   return mmseq_check_launch("conv_im2col");
 }
@@ -478,17 +632,24 @@ extern "C" mmseq_status mmseq_conv_col2im(int U, int H, int W, int C, int ks, in
   if (U == 0) return MMSEQ_OK;
   ConvGeom g{U, H, W, C, (H + 2 * pad - ks) / stride + 1, (W + 2 * pad - ks) / stride + 1, ks,
              stride, pad, Kp};
-  const int64_t n = (int64_t)U * H * W * C;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define LAUNCH(T, _) hipLaunchKernelGGL(col2im_nhwc_kernel<T>, dim3(blocks<T>(n)), dim3(256), 0, s, \
-                                        g, (const T*)dcols, (T*)dx)
+  const bool vec = C % 8 == 0 && Kp % 8 == 0 && (((uintptr_t)dcols | (uintptr_t)dx) & 15) == 0;
+  const int64_t n = (int64_t)U * H * W * (vec ? C / 8 : C);
+  const dim3 grid((unsigned)((n + 255) / 256));
+#define LAUNCH(T, _)                                                                          \
+  if (vec)                                                                                    \
+    hipLaunchKernelGGL((col2im_nhwc_kernel<T, 8>), grid, dim3(256), 0, s, g, (const T*)dcols, \
+                       (T*)dx);                                                               \
+  else                                                                                        \
+    hipLaunchKernelGGL((col2im_nhwc_kernel<T, 1>), grid, dim3(256), 0, s, g, (const T*)dcols, (T*)dx)
   MMSEQ_DT_DISPATCH(dtype, LAUNCH, 0);
 #undef LAUNCH
   return mmseq_check_launch("conv_col2im");
 }
 
 extern "C" int64_t mmseq_bn_workspace(int64_t rows, int C) {
-  return (3 * ((rows + kChunk - 1) / kChunk) * (int64_t)C + 2 * (int64_t)C) * (int64_t)sizeof(float);
+  if (rows < 0 || C <= 0 || !bn_shape_ok(C)) return 0;
+  return (3 * (int64_t)bn_plan(rows, C).nch * C + 2 * (int64_t)C) * (int64_t)sizeof(float);
 }
 
 extern "C" mmseq_status mmseq_bn_fwd(int64_t rows, int C, const void* x, const float* gamma,
@@ -497,31 +658,33 @@ extern "C" mmseq_status mmseq_bn_fwd(int64_t rows, int C, const void* x, const f
                                      float* rstd, float* run_mean, float* run_var, void* y,
                                      float* workspace, int64_t workspace_bytes,
                                      mmseq_dtype dtype, mmseq_stream stream) {
-  MMSEQ_REQUIRE(rows >= 0 && C > 0 && (C % 64 == 0 || (C <= 64 && 64 % C == 0)),
-                "bn_fwd: C must be a multiple of 64 or divide 64");
+  MMSEQ_REQUIRE(rows >= 0 && C > 0 && bn_shape_ok(C),
+                "bn_fwd: C must be 8 x a power of two up to 512, or a multiple of 512");
   MMSEQ_REQUIRE(x && gamma && beta && mean && rstd && y, "bn_fwd: null buffer");
   MMSEQ_REQUIRE(train || (run_mean && run_var), "bn_fwd: eval needs running statistics");
+  MMSEQ_REQUIRE((((uintptr_t)x | (uintptr_t)resid | (uintptr_t)y | (uintptr_t)mean |
+                  (uintptr_t)rstd | (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0,
+                "bn_fwd: buffers must be 16-byte aligned");
   if (rows == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (train) {
     MMSEQ_REQUIRE(workspace && workspace_bytes >= mmseq_bn_workspace(rows, C),
                   "bn_fwd: workspace too small");
-    const int nch = (int)((rows + kChunk - 1) / kChunk);
-    const dim3 grid(C < 64 ? 1 : C / 64, nch);
-#define LAUNCH(T, _) hipLaunchKernelGGL(bn_stats_partial_kernel<T>, grid, dim3(256), 0, s, rows, C, \
-                                        (const T*)x, workspace)
+    const BnPlan pl = bn_plan(rows, C);
+#define LAUNCH(T, _) hipLaunchKernelGGL(bn_stats_partial_kernel<T>, dim3(pl.gx, pl.nch), dim3(256), 0, \
+                                        s, rows, C, pl, (const T*)x, workspace)
     MMSEQ_DT_DISPATCH(dtype, LAUNCH, 0);
 #undef LAUNCH
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, nch,
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, C, pl.nch,
                        workspace, eps, momentum, n_ref, mean, rstd, run_mean, run_var);
   } else {
     // eval: the running statistics, as mean / rstd for the apply and the backward
     hipLaunchKernelGGL(bn_eval_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, eps,
                        run_mean, run_var, mean, rstd);
   }
-  const int64_t n = rows * C;
+  const int64_t n8 = rows * C / 8;
 #define LAUNCH(T, _)                                                                        \
-  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(blocks<T>(n)), dim3(256), 0, s, n, C,          \
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3((n8 + 255) / 256), dim3(256), 0, s, n8, C,     \
                      (const T*)x, mean, rstd, gamma, beta, (const T*)resid, relu, (T*)y)
   MMSEQ_DT_DISPATCH(dtype, LAUNCH, 0);
 #undef LAUNCH
@@ -534,25 +697,27 @@ extern "C" mmseq_status mmseq_bn_bwd(int64_t rows, int C, const void* dy, const 
                                      void* dx, void* dres, float* workspace,
                                      int64_t workspace_bytes, mmseq_dtype dtype,
                                      mmseq_stream stream) {
-  MMSEQ_REQUIRE(rows >= 0 && C > 0 && (C % 64 == 0 || (C <= 64 && 64 % C == 0)),
-                "bn_bwd: C must be a multiple of 64 or divide 64");
+  MMSEQ_REQUIRE(rows >= 0 && C > 0 && bn_shape_ok(C),
+                "bn_bwd: C must be 8 x a power of two up to 512, or a multiple of 512");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "bn_bwd: null buffer");
   MMSEQ_REQUIRE(workspace_bytes >= mmseq_bn_workspace(rows, C), "bn_bwd: workspace too small");
+  MMSEQ_REQUIRE((((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)dres |
+                  (uintptr_t)mean | (uintptr_t)rstd | (uintptr_t)gamma | (uintptr_t)workspace) &
+                 15) == 0, "bn_bwd: buffers must be 16-byte aligned");
   if (rows == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int nch = (int)((rows + kChunk - 1) / kChunk);
-  float* sums = workspace + 3 * (int64_t)nch * C;
-  const dim3 grid(C < 64 ? 1 : C / 64, nch);
-#define LAUNCH(T, _) hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, grid, dim3(256), 0, s, rows, C,   \
-                                        (const T*)dy, (const T*)y, (const T*)x, mean, rstd,     \
-                                        workspace)
+  const BnPlan pl = bn_plan(rows, C);
+  float* sums = workspace + 3 * (int64_t)pl.nch * C;
+#define LAUNCH(T, _) hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, dim3(pl.gx, pl.nch), dim3(256), 0, \
+                                        s, rows, C, pl, (const T*)dy, (const T*)y, (const T*)x, \
+                                        mean, rstd, workspace)
   MMSEQ_DT_DISPATCH(dtype, LAUNCH, 0);
 #undef LAUNCH
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, nch,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, C, pl.nch,
                      workspace, sums, dgamma, dbeta);
-  const int64_t n = rows * C;
-#define LAUNCH(T, _)                                                                        \
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks<T>(n)), dim3(256), 0, s, n, C, rows, \
+  const int64_t n8 = rows * C / 8;
+#define LAUNCH(T, _)                                                                          \
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3((n8 + 255) / 256), dim3(256), 0, s, n8, C, rows, \
                      (const T*)dy, (const T*)y, (const T*)x, mean, rstd, gamma, sums, train,   \
                      (T*)dx, (T*)dres)
   MMSEQ_DT_DISPATCH(dtype, LAUNCH, 0);

@@ -154,3 +154,121 @@ def test_rn50_bf16_close_to_reference():
                 continue
             cos = float(a @ b / (a.norm() * b.norm() + 1e-30))
             assert cos > 0.95, (k, cos)
+
+
+# ------------------------------------------------------------------------------------------------
+# the RN50 primitives against plain torch fp32 (every im2col mode, narrow and wide BatchNorm)
+
+def _unfold_nhwc(x, ks, stride, pad, Kp):
+    """reference columns [U*Ho*Wo][Kp] in (ky, kx, c) order from torch's unfold"""
+    U, H, W, C = x.shape
+    u = torch.nn.functional.unfold(x.permute(0, 3, 1, 2).float(), ks, padding=pad, stride=stride)
+    L = u.shape[-1]
+    u = u.view(U, C, ks * ks, L).permute(0, 3, 2, 1).reshape(U * L, ks * ks * C)
+    return torch.nn.functional.pad(u, (0, Kp - ks * ks * C))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("U,H,C,ks,stride,Kp", [(3, 19, 3, 3, 2, 32), (2, 14, 16, 3, 1, 192),
+                                                 (2, 9, 5, 3, 1, 45), (2, 8, 64, 3, 1, 576)])
+def test_conv_im2col_col2im_match_torch(dtype, U, H, C, ks, stride, Kp):
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator().manual_seed(H * C)
+    x = torch.randn(U, H, H, C, generator=g).to(dtype).cuda()
+    pad = (ks - 1) // 2
+    Ho = (H + 2 * pad - ks) // stride + 1
+    cols = torch.full((U * Ho * Ho, Kp), 7.0, dtype=dtype, device="cuda")
+    N.conv_im2col(x, ks, stride, pad, Kp, cols)
+    torch.testing.assert_close(cols.float().cpu(), _unfold_nhwc(x.cpu(), ks, stride, pad, Kp),
+                               rtol=0, atol=0)
+    # col2im is the adjoint: fold of the columns (padding columns ignored)
+    dcols = torch.randn(U * Ho * Ho, Kp, generator=g).to(dtype).cuda()
+    dx = torch.empty_like(x)
+    N.conv_col2im(dcols, U, H, H, C, ks, stride, pad, Kp, dx)
+    d = dcols.float().cpu()[:, :ks * ks * C].view(U, Ho * Ho, ks * ks, C).permute(0, 3, 2, 1)
+    ref = torch.nn.functional.fold(d.reshape(U, C * ks * ks, Ho * Ho), (H, H), ks, padding=pad,
+                                   stride=stride).permute(0, 2, 3, 1)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dx.float().cpu(), ref, **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(3, 32), (777, 32), (50000, 64), (3001, 256), (4099, 1024),
+                                    (200, 2048), (9000, 8)])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_batchnorm_train_matches_torch(dtype, rows, C, relu, res):
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator().manual_seed(rows + C)
+    x = (torch.randn(rows, C, generator=g) * 3 + 5).to(dtype)
+    r = torch.randn(rows, C, generator=g).to(dtype) if res else None
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    dy = torch.randn(rows, C, generator=g).to(dtype)
+    # torch fp32 reference (BatchNorm1d over rows = BatchNorm2d over N*H*W)
+    xr = x.float().clone().requires_grad_()
+    gr, br = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    rr = r.float().clone().requires_grad_() if res else None
+    rmr, rvr = rm.clone(), rv.clone()
+    yr = torch.nn.functional.batch_norm(xr, rmr, rvr, gr, br, training=True, momentum=0.1,
+                                        eps=1e-5)
+    if res:
+        yr = yr + rr
+    # device
+    dev = lambda t: None if t is None else t.cuda()  # noqa: E731
+    xd, rd, gd, bd, rmd, rvd = map(dev, (x, r, gamma, beta, rm.clone(), rv.clone()))
+    mean, rstd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    y = torch.empty_like(xd)
+    N.bn_fwd(xd, gd, bd, rd, relu, True, 1e-5, 0.1, rows, mean, rstd, rmd, rvd, y)
+    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dx = torch.empty_like(xd)
+    dres = torch.empty_like(xd) if res else None
+    N.bn_bwd(dy.cuda(), y if relu else None, xd, mean, rstd, gd, True, dg, db, dx, dres)
+    torch.cuda.synchronize()
+    f32 = dtype == torch.float32
+    tol = dict(rtol=1e-4, atol=1e-4) if f32 else dict(rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(y.float().cpu(), yr.detach().relu() if relu else yr.detach(), **tol)
+    # backward through the device's ReLU gate: an output within rounding of 0 may sit on either
+    # side of it, and a flipped gate moves that element's gradient by dy * xhat
+    (yr * (y.float().cpu() > 0) if relu else yr).backward(dy.float())
+    torch.testing.assert_close(rmd.cpu(), rmr, rtol=1e-5, atol=1e-5)
+    if rows > 1:
+        torch.testing.assert_close(rvd.cpu(), rvr, rtol=1e-4, atol=1e-5)
+    gtol = dict(rtol=1e-3, atol=1e-3 * max(1.0, rows ** 0.5) / 10) if f32 else \
+        dict(rtol=5e-2, atol=5e-2 * max(1.0, rows ** 0.5) / 10)
+    torch.testing.assert_close(dg.cpu(), gr.grad, **gtol)
+    torch.testing.assert_close(db.cpu(), br.grad, **gtol)
+    if rows > 1:
+        torch.testing.assert_close(dx.float().cpu(), xr.grad, **(dict(rtol=1e-3, atol=1e-3) if f32
+                                                                  else dict(rtol=5e-2, atol=5e-2)))
+    if res:
+        torch.testing.assert_close(dres.float().cpu(), rr.grad, **tol)
+
+
+@pytest.mark.gpu
+def test_batchnorm_rejects_unsupported_channels():
+    from multimodal_sequencing_amd import _native as N
+    x = torch.zeros(10, 40, device="cuda")
+    c = torch.zeros(40, device="cuda")
+    with pytest.raises(RuntimeError, match="bn_fwd"):
+        N.bn_fwd(x, c, c, None, True, True, 1e-5, 0.1, 10, c.clone(), c.clone(), c.clone(),
+                 c.clone(), torch.empty_like(x))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_avgpool2_matches_torch(dtype):
+    from multimodal_sequencing_amd import _native as N
+    x = torch.randn(3, 14, 14, 24).to(dtype).cuda()
+    y = torch.empty(3, 7, 7, 24, dtype=dtype, device="cuda")
+    N.avgpool2(x, y)
+    ref = torch.nn.functional.avg_pool2d(x.float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    tol = dict(rtol=1e-6, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(y.float(), ref, **tol)
+    dy = torch.randn(3, 7, 7, 24).to(dtype).cuda()
+    dx = torch.empty_like(x)
+    N.avgpool2(dy, dx, backward=True)
+    torch.testing.assert_close(dx.float(), dy.float().repeat_interleave(2, 1).repeat_interleave(2, 2)
+                               * 0.25, **tol)
