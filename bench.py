@@ -530,6 +530,9 @@ def main():
         "model_flops_util": stories / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
         "loss": float(loss.item()) if loss is not None else None,
     }
+    _mpk, _ = measured_peak()
+    if _mpk:  # stories/s x (fwd+bwd FLOP/story) / measured peak
+        out["model_flops_util_of_measured_peak"] = stories / dt * 3 * fwd / 1e12 / _mpk
     if fwd_dt is not None:
         fst = args.batch * args.fwd_steps * world / fwd_dt
         mpk, _src = measured_peak()
@@ -578,6 +581,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config)
+            out["cpu_baseline"]["tflops"] = out["cpu_baseline"]["value"] * 3 * fwd / 1e12
         except Exception as e:  # the baseline is reported, never required for the GPU number
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
