@@ -256,9 +256,9 @@ def gemm_set_fast(variant):
 
 
 def attn_set_fast(variant):
-    """bf16 attention variant passed by this binding: 2 = 32x32x16-MFMA forward (product),
-    1 = 128-row 16x16x32 LDS-DMA pipelined kernels, 0 = the 64-row kernels (cross-checks in the
-    tests). The backward uses the 128-row kernels for any nonzero variant."""
+    """bf16 attention variant passed by this binding: 1 = 128-row 16x16x32 LDS-DMA pipelined
+    kernels (product), 2 = 32x32x16-MFMA forward (measured, not faster), 0 = the 64-row kernels
+    (cross-checks in the tests). The backward uses the 128-row kernels for any nonzero variant."""
     _sel["attn"] = int(variant)
 
 

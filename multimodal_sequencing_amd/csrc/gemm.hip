@@ -48,6 +48,7 @@ struct GemmSel {
   int big;            // 256 x 256 NT / TN kernels: 1 for large problems, 2 always, 0 never
   bool ring;          // BK=32 four-slot ring kernel instead of the BK=64 double-buffer kernel
   int nt_variant;     // large NT: 0 = 256x256 one block/CU, 1 = 256x128 two blocks/CU
+  int nt_delay;       // large NT: start delay (cycles) of the blocks with one tile fewer
   int num_cu;
 };
 
@@ -57,6 +58,7 @@ static bool make_sel(int variant, GemmSel* s) {
   s->big = variant == 1 ? 1 : ((variant == 4 || variant == 5) ? 2 : 0);
   s->nt_variant = variant == 5 ? 1 : 0;
   s->ring = variant == 3;
+  s->nt_delay = 0;
   s->num_cu = device_cus();
   return true;
 }
@@ -673,7 +675,7 @@ hipError_t launch_fast(int trans, const GemmArgs& a, int batch, hipStream_t s, c
   if (!trans && sel.big && a.splitk == 1 && batch == 1 && a.K % 128 == 0 &&
       (sel.big == 2 || (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256)) {
     hipError_t e;
-    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, sel.num_cu, s, &e, sel.nt_variant)) return e;
+    if (mmseq_gemm256_nt(a, sizeof(TO) == 2, sel.num_cu, s, &e, sel.nt_variant, sel.nt_delay)) return e;
   }
   const int tiles_m = (a.M + 127) / 128, tiles_n = (a.N + 127) / 128;
   dim3 grid(tiles_m * tiles_n, a.splitk > 1 ? a.splitk : batch);

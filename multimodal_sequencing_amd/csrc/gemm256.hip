@@ -149,7 +149,8 @@ __device__ __forceinline__ int g8_of(int X, int q) {
 }
 
 template <int ACT, bool BWD, bool XIN>
-__global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles) {
+__global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles,
+                                                            int delay) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF];  // 128 KB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -158,6 +159,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   // XCD-aware order: the G/8 blocks sharing an XCD take consecutive tiles (shared A panels in L2)
   const int bid = blockIdx.x;
   const int first = xcd_item(bid, G);
+  // Epilogue de-synchronisation: the blocks with one tile fewer than the busiest ones have that
+  // tile's time as slack; they start `delay` shader cycles late, so their epilogue store bursts
+  // fall in the other blocks' main loops instead of all CUs storing at once.
+  if (delay > 0 && first < ntiles && (ntiles - 1 - first) / G < (ntiles - 1) / G) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)delay) __builtin_amdgcn_s_sleep(8);
+  }
   const int nk = a.K >> 6;
   const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
   const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);
@@ -603,7 +611,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
 constexpr int S2_STAGE = 256 * 32 + 128 * 32;  // elements per stage
 
 template <int ACT, bool BWD, bool XIN>
-__global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tiles_n, int ntiles) {
+__global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tiles_n, int ntiles,
+                                                             int /*delay: unused*/) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[3 * S2_STAGE];  // 72 KB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -734,7 +743,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tile
 }  // namespace
 
 bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s, hipError_t* err,
-                      int variant) {
+                      int variant, int delay) {
   auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!out_bf16 || a.K % 128 != 0 || a.splitk != 1 || a.N % 8 != 0 || a.ldc % 8 != 0 ||
       (a.accumulate && (a.resid || a.dact)) ||
@@ -748,19 +757,19 @@ bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t 
 #define NT_DISPATCH(KERNEL, GRID, BLOCK)                                                            \
   switch (a.act) {                                                                                  \
     case 0:                                                                                         \
-      if (noepi) hipLaunchKernelGGL((KERNEL<-1, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);  \
-      else if (xin) hipLaunchKernelGGL((KERNEL<0, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles); \
-      else hipLaunchKernelGGL((KERNEL<0, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);         \
+      if (noepi) hipLaunchKernelGGL((KERNEL<-1, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);  \
+      else if (xin) hipLaunchKernelGGL((KERNEL<0, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay); \
+      else hipLaunchKernelGGL((KERNEL<0, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);         \
       break;                                                                                        \
     case MMSEQ_ACT_GELU_ERF:                                                                        \
-      if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles);        \
-      else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles); \
-      else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);         \
+      if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);        \
+      else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay); \
+      else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_GELU_ERF, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);         \
       break;                                                                                        \
     default:                                                                                        \
-      if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles);        \
-      else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles); \
-      else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles);         \
+      if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);        \
+      else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay); \
+      else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);         \
   }
   if (variant == 1 && a.K % 32 == 0) {  // two 256 x 128 blocks per CU
     const int tn = (a.N + 127) / 128;

@@ -110,9 +110,10 @@ __device__ __forceinline__ void dma16(rsrc_t r, unsigned short* lds, uint32_t vo
 }  // namespace mmseq_gemm_detail
 
 // persistent 256 x 256 NT kernel (gemm256.hip); returns false when its preconditions fail
-// variant 0: one 8-wave 256 x 256 block per CU; 1: two 4-wave 256 x 128 blocks per CU
+// variant 0: one 8-wave 256 x 256 block per CU; 1: two 4-wave 256 x 128 blocks per CU.
+// delay: shader cycles by which the blocks with one tile fewer start late (0: none)
 bool mmseq_gemm256_nt(const mmseq_gemm_detail::GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s,
-                      hipError_t* err, int variant);
+                      hipError_t* err, int variant, int delay);
 // 256 x 256 TN (wgrad) kernel, fp32 out: a.splitk / a.kchunk (multiple of 128) / a.slab set by the
 // caller (slab [splitk][M][N] when splitk > 1); returns false when its preconditions fail
 bool mmseq_gemm256_tn(const mmseq_gemm_detail::GemmArgs& a, hipStream_t s, hipError_t* err);
