@@ -1361,29 +1361,20 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     if (!active) continue;
     const unsigned short* qimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* oimg = qimg + IMG;
-    // dropout keep-bits of this lane's 32 (q, key) elements, bit grp*16 + qs*4 + r, computed
-    // before the MFMAs (few live registers); (q, key) -> index (rb + q) * Tp2 + key
+    // dropout multiplier of element (grp, qs, r): 0 or 1/(1-p), as the bits of the scale ANDed with
+    // a sign-extended 1-bit field (v_bfe_i32 + v_and per element)
+    const uint32_t scale_u = __float_as_uint(a.drop.scale);
+    // DMODE 2: word (kt0 + (wave >> 1)) of a row holds this wave's keys; key j (0..63 in its
+    // tile) sits at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3) (16-bit slice per forward lane
+    // group). With j = (wave & 1) * 32 + grp * 16 + i that bit is in dword (i >> 3) & 1 of the word
+    // at position pos0 + 4 grp: one 32-bit LDS read per query serves both groups, and the element's
+    // multiplier is extracted straight from it
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(sBits + (t & 1) * 512) +
+                         (wave >> 1) * 2 + ((i >> 3) & 1);
+    const uint32_t pos0 = ((i >> 2) & 1) * 16 + (wave & 1) * 8 + (i & 3);
+    // DMODE 1: keep bits of this lane's 32 (q, key) elements, bit grp*16 + qs*4 + r, hashed before
+    // the MFMAs (few live registers); (q, key) -> index (rb + q) * Tp2 + key
     uint32_t keep = 0xFFFFFFFFu;
-    if (DMODE == 2) {
-      // word (kt0 + (wave >> 1)) of a row holds this wave's keys; key j (0..63 in its tile) sits
-      // at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 + (j & 3) (16-bit slice per forward lane group)
-      // With j = (wave & 1) * 32 + grp * 16 + i that bit is in dword (i >> 3) & 1 of the word at
-      // position ((i >> 2) & 1) * 16 + ((wave & 1) * 2 + grp) * 4 + (i & 3): one 32-bit LDS read
-      // per query serves both groups, one bit-field extract per element
-      keep = 0;
-      const uint32_t* bw = reinterpret_cast<const uint32_t*>(sBits + (t & 1) * 512) +
-                           (wave >> 1) * 2 + ((i >> 3) & 1);
-      const uint32_t pos0 = ((i >> 2) & 1) * 16 + (wave & 1) * 8 + (i & 3);
-#pragma unroll
-      for (int qs = 0; qs < 4; ++qs)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t w = bw[(qs * 16 + 4 * g + r) * 4];
-#pragma unroll
-          for (int grp = 0; grp < 2; ++grp)
-            keep |= __builtin_amdgcn_ubfe(w, pos0 + 4 * grp, 1) << (grp * 16 + qs * 4 + r);
-        }
-    }
     if (DMODE == 1) {
       keep = 0;
       const uint64_t dbase = (uint64_t)(rb + t * 64 + 4 * g) * (uint64_t)Tp2 + kw + i;
@@ -1405,6 +1396,13 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     // P / dS, then dV^T[d][key] += dO^T[d][q] P[q][key] and dK^T[d][key] += Q^T[d][q] dS[q][key]
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      uint32_t kw32[2][4];  // DMODE 2: keep words of queries (2ks + h2) * 16 + 4g + r
+      if (DMODE == 2) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kw32[h2][r] = bw[((2 * ks + h2) * 16 + 4 * g + r) * 4];
+      }
       f32x4 s[2][2], dp[2][2];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
@@ -1430,7 +1428,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
           for (int r = 0; r < 4; ++r) {
             const float pv = ex2(fmaf(s[grp][h2][r], c, kb2[grp]) - Lq[r]);
             float mk = 1.f;
-            if (DROP) mk = ((keep >> (grp * 16 + qs * 4 + r)) & 1u) ? a.drop.scale : 0.f;
+            if (DMODE == 2)
+              mk = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw32[h2][r], pos0 + 4 * grp, 1) & scale_u);
+            if (DMODE == 1) mk = ((keep >> (grp * 16 + qs * 4 + r)) & 1u) ? a.drop.scale : 0.f;
             s[grp][h2][r] = pv * mk;
             dp[grp][h2][r] = pv * fmaf(dp[grp][h2][r], mk, -Dq[r]);
           }

@@ -48,12 +48,13 @@ int main() {
     const double fl = 2.0 * R * N * K;
     const int est_tile = 73 * K;  // shader cycles per 256x256 tile at ~1.1 PFLOP/s (estimate)
     struct Cfg { const char* name; int epi; int cus; float frac; };
+    // epi: 0 none, 1 plain, 2 residual. (A probe of 8 rows x 128 B per store instruction instead
+    // of 16 x 64 B measured equal to plain: profiles/r2s2_gemm_store_shape.json.)
     std::vector<Cfg> cfgs = {{"noepi", 0, dev_cus, 0.f},      {"plain", 1, dev_cus, 0.f},
-                             {"resid", 2, dev_cus, 0.f},      {"noepi_half", 0, dev_cus / 2, 0.f},
-                             {"plain_half", 1, dev_cus / 2, 0.f}, {"resid_half", 2, dev_cus / 2, 0.f},
+                             {"resid", 2, dev_cus, 0.f},      {"noepi_halfcu", 0, dev_cus / 2, 0.f},
+                             {"plain_halfcu", 1, dev_cus / 2, 0.f}, {"resid_halfcu", 2, dev_cus / 2, 0.f},
                              {"plain_d25", 1, dev_cus, .25f}, {"plain_d50", 1, dev_cus, .5f},
-                             {"plain_d75", 1, dev_cus, .75f}, {"resid_d25", 2, dev_cus, .25f},
-                             {"resid_d50", 2, dev_cus, .5f},  {"resid_d75", 2, dev_cus, .75f}};
+                             {"resid_d25", 2, dev_cus, .25f}, {"resid_d50", 2, dev_cus, .5f}};
     printf("{\"N\": %d, \"K\": %d, \"tiles\": %d", N, K, ((R + 255) / 256) * (N / 256));
     for (auto& c : cfgs) {
       mmseq_gemm_detail::GemmArgs a{};
