@@ -32,7 +32,8 @@ def main():
                 per[g][r.get("Dispatch_Id") or r.get("Correlation_Id")][r["Counter_Name"]] = \
                     float(r["Counter_Value"])
     out = {"cus": cus, "source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE "
-                                 "SQ_BUSY_CYCLES, bench.py --steps 1 --warmup 1",
+                                 "SQ_BUSY_CYCLES, bench.py (default config-3 workload) --steps 1 "
+                                 "--warmup 1 via tools/profile_round.sh",
            "definition": "MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 4 SIMD * CUs), per dispatch, averaged"}
     for g, disp in per.items():
         utils = []

@@ -40,7 +40,7 @@ def main():
     write = load(sys.argv[2], "WRITE_SIZE")
     out = {"units": "bytes per launch", "fetch_correction": 2.0,
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
-                     "bench.py --steps 1 --warmup 0"}
+                     "bench.py (default config-3 workload) --steps 1 --warmup 0 via tools/profile_round.sh"}
     for g in GROUPS:
         if not fetch.get(g) or not write.get(g):
             continue
