@@ -3,6 +3,8 @@ import json, os, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodal_sequencing_amd import _native as N
+if os.environ.get("MMSEQ_BENCH_LIB"):  # A/B runs: another build of the library, same process layout
+    N.LIB_PATH = os.environ["MMSEQ_BENCH_LIB"]
 
 
 def run(P, T, heads, drop, iters=5, bits=False, variant=1):
