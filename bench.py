@@ -33,6 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from multimodal_sequencing_amd import _native as N  # noqa: E402
+if os.environ.get("MMSEQ_BENCH_LIB"):  # A/B runs on one box: another build of the library
+    N.LIB_PATH = os.environ["MMSEQ_BENCH_LIB"]
 from multimodal_sequencing_amd import kernels as K  # noqa: E402
 from multimodal_sequencing_amd import model_zoo  # noqa: E402
 from multimodal_sequencing_amd.trainer import (FusedAdamW, GradAllReduce,  # noqa: E402

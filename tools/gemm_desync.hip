@@ -54,7 +54,11 @@ int main() {
                              {"resid", 2, dev_cus, 0.f},      {"noepi_halfcu", 0, dev_cus / 2, 0.f},
                              {"plain_halfcu", 1, dev_cus / 2, 0.f}, {"resid_halfcu", 2, dev_cus / 2, 0.f},
                              {"plain_d25", 1, dev_cus, .25f}, {"plain_d50", 1, dev_cus, .5f},
-                             {"resid_d25", 2, dev_cus, .25f}, {"resid_d50", 2, dev_cus, .5f}};
+                             {"resid_d25", 2, dev_cus, .25f}, {"resid_d50", 2, dev_cus, .5f},
+                             // grid a multiple of the column-tile count (252 = 28 x 9 = 84 x 3 =
+                             // 21 x 12): every block keeps its B panel from round to round
+                             {"noepi_g252", 0, 252, 0.f}, {"plain_g252", 1, 252, 0.f},
+                             {"resid_g252", 2, 252, 0.f}};
     printf("{\"N\": %d, \"K\": %d, \"tiles\": %d", N, K, ((R + 255) / 256) * (N / 256));
     for (auto& c : cfgs) {
       mmseq_gemm_detail::GemmArgs a{};
