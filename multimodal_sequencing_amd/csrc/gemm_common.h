@@ -35,14 +35,18 @@ __device__ __forceinline__ void epilogue4(const GemmArgs& a, TO* __restrict__ C,
     const TO* dp = dact + (int64_t)m * a.ldc + n;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (n + r < a.N) v[r] *= act_bwd(a.act, Elem<TO>::ld(dp + r));
+      if (n + r < a.N)
+        v[r] *= sizeof(TO) == 2 ? act_bwd_fast(a.act, Elem<TO>::ld(dp + r))
+                                : act_bwd(a.act, Elem<TO>::ld(dp + r));
   } else if (a.act) {
     TO* ap = aux ? aux + (int64_t)m * a.ldc + n : nullptr;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (n + r < a.N) {
         if (ap) Elem<TO>::st(ap + r, v[r]);
-        v[r] = act_fwd(a.act, v[r]);
+        // bf16 out: branch-free erf (|error| <= 1.5e-7, far below bf16 resolution); the fp32
+        // parity path keeps libm's erff
+        v[r] = sizeof(TO) == 2 ? act_fwd_fast(a.act, v[r]) : act_fwd(a.act, v[r]);
       }
     }
   }

@@ -9,6 +9,9 @@ import torch
 
 sys.path.insert(0, ".")
 from multimodal_sequencing_amd import _native as N  # noqa: E402
+import os  # noqa: E402
+if os.environ.get("MMSEQ_BENCH_LIB"):  # A/B runs on one box: another build of the library
+    N.LIB_PATH = os.environ["MMSEQ_BENCH_LIB"]
 
 
 def timeit(fn, reps=10):
@@ -27,16 +30,16 @@ def main():
     M = int(sys.argv[1]) if len(sys.argv) > 1 else 72 * 769
     dev = "cuda"
     out = {"rows": M, "shapes": []}
-    for name, Nn, K in [("qkv", 3072, 1024), ("o", 1024, 1024), ("fc1", 4096, 1024),
-                        ("fc2", 1024, 4096)]:
+    for name, Nn, K, act in [("qkv", 3072, 1024, 0), ("o", 1024, 1024, 0), ("fc1", 4096, 1024, 0),
+                             ("fc1_gelu", 4096, 1024, 1), ("fc2", 1024, 4096, 0)]:
         A = torch.randn(M, K, device=dev).bfloat16()
         W = (torch.randn(Nn, K, device=dev) * 0.02).bfloat16()
         bias = torch.zeros(Nn, device=dev)
         C = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
-        t_bf16 = timeit(lambda: N.gemm(A, W, C, M, Nn, K, bias=bias))
+        t_bf16 = timeit(lambda: N.gemm(A, W, C, M, Nn, K, bias=bias, act=act))
         qa, qw = N.quant_mxfp8(A), N.quant_mxfp8(W)
         t_q = timeit(lambda: N.quant_mxfp8(A, out=qa))
-        t_fp8 = timeit(lambda: N.gemm_mxfp8(qa, qw, C, bias=bias))
+        t_fp8 = timeit(lambda: N.gemm_mxfp8(qa, qw, C, bias=bias, act=act))
         fl = 2.0 * M * Nn * K
         out["shapes"].append({"gemm": name, "N": Nn, "K": K,
                               "bf16_us": t_bf16 * 1e6, "bf16_tflops": fl / t_bf16 / 1e12,
