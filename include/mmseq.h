@@ -379,6 +379,14 @@ mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int64_t lda,
                               const void* b_scales, void* C, int64_t ldc, const float* bias,
                               int act, const void* resid, int64_t ldr, float alpha,
                               mmseq_stream stream);
+/* gemm_mxfp8_out: bf16 GEMM whose output is written in the format above, for a consumer GEMM
+ *  that takes it as its MX-fp8 A operand (the MLP: FC1 + GELU -> FC2, lxrt/modeling.py:467-493)
+ *  with no quantisation pass: q [M][N] e4m3 (ldq % 16 == 0) + scales for (M, N) =
+ *  quant(bf16(act(A B^T + bias))), bit-identical to mmseq_gemm (bf16 out) + mmseq_quant_mxfp8.
+ *  A [M][K], B [N][K] bf16, K % 128 == 0, N % 32 == 0, 16-byte aligned operands. */
+mmseq_status mmseq_gemm_mxfp8_out(int M, int N, int K, const void* A, int64_t lda, const void* B,
+                                  int64_t ldb, const float* bias, int act, void* q, int64_t ldq,
+                                  void* scales, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * CLIP ModifiedResNet / RN50 (clip/model.py:10-187; lxrt/modeling.py:621-705, 1014-1030), NHWC.

@@ -127,6 +127,9 @@ _SIGS = {
     "mmseq_gemm_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
                                                             _vp, _c_i64, _vp, ctypes.c_int, _vp,
                                                             _c_i64, ctypes.c_float, _vp]),
+    "mmseq_gemm_mxfp8_out": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _c_i64, _vp,
+                                                                ctypes.c_int, _vp, _c_i64, _vp,
+                                                                _vp]),
     "mmseq_conv_im2col": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_conv_col2im": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_bn_workspace": (ctypes.c_int64, [_c_i64, ctypes.c_int]),
@@ -524,6 +527,21 @@ def gemm_mxfp8(a, b, c, bias=None, act=0, resid=None, alpha=1.0):
                                   _p(bias), act, _p(resid),
                                   resid.stride(0) if resid is not None else 0, alpha, _stream()),
            "mmseq_gemm_mxfp8")
+
+
+def gemm_mxfp8_out(x, W, bias=None, act=0):
+    """MXFP8 of bf16(act(x @ W^T + bias)) (x [rows][K], W [N][K] bf16) straight from the GEMM
+    epilogue (mmseq_gemm_mxfp8_out): the consumer GEMM's A operand without a quantisation pass."""
+    rows, K = x.shape
+    Nn = W.shape[0]
+    if x.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or W.shape[1] != K:
+        raise ValueError("gemm_mxfp8_out: bf16 x [rows][K], W [N][K]")
+    q = torch.empty(rows, (Nn + 15) // 16 * 16, dtype=torch.uint8, device=x.device)
+    sc = torch.empty(lib().mmseq_mxfp8_scale_bytes(rows, Nn), dtype=torch.uint8, device=x.device)
+    _check(lib().mmseq_gemm_mxfp8_out(rows, Nn, K, _p(x), x.stride(0), _p(W), W.stride(0),
+                                      _p(bias), act, _p(q), q.stride(0), _p(sc), _stream()),
+           "mmseq_gemm_mxfp8_out")
+    return MXFP8(q, sc, rows, Nn)
 
 
 # -- RN50 (csrc/resnet.hip) ----------------------------------------------------------------------

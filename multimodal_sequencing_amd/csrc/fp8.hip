@@ -252,3 +252,30 @@ extern "C" mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int
                      mmseq_mxfp8_scale_bytes(N, K), tiles_n);
   return mmseq_check_launch("gemm_mxfp8");
 }
+
+extern "C" mmseq_status mmseq_gemm_mxfp8_out(int M, int N, int K, const void* A, int64_t lda,
+                                             const void* B, int64_t ldb, const float* bias,
+                                             int act, void* q, int64_t ldq, void* scales,
+                                             mmseq_stream stream) {
+  MMSEQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 128 == 0 && N % 32 == 0,
+                "gemm_mxfp8_out: K % 128 and N % 32 must be 0");
+  MMSEQ_REQUIRE(lda >= K && ldb >= K && lda % 8 == 0 && ldb % 8 == 0 && ldq >= N && ldq % 16 == 0,
+                "gemm_mxfp8_out: leading dimensions");
+  MMSEQ_REQUIRE(A && B && q && scales, "gemm_mxfp8_out: null buffer");
+  MMSEQ_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && ((uintptr_t)q & 15) == 0,
+                "gemm_mxfp8_out: 16-byte alignment");
+  MMSEQ_REQUIRE(act == 0 || act == MMSEQ_ACT_GELU_ERF || act == MMSEQ_ACT_QUICKGELU,
+                "gemm_mxfp8_out: act");
+  if (M == 0) return MMSEQ_OK;
+  GemmArgs a{};
+  a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = q; a.ldc = ldq;
+  a.bias = bias; a.act = act; a.alpha = 1.f; a.splitk = 1; a.kchunk = K;
+  a.drop = make_drop(nullptr);
+  a.q8_scales = reinterpret_cast<uint8_t*>(scales);
+  hipError_t e = hipSuccess;
+  MMSEQ_REQUIRE(mmseq_gemm256_nt_q8(a, mmseq_device_cus(), reinterpret_cast<hipStream_t>(stream), &e),
+                "gemm_mxfp8_out: preconditions");
+  if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_mxfp8_out launch: %s", hipGetErrorString(e));
+  return mmseq_check_launch("gemm_mxfp8_out");
+}

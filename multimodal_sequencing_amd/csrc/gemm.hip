@@ -41,6 +41,7 @@ static int device_cus() {
   g_cu_table[dev].store(n, std::memory_order_relaxed);
   return n;
 }
+int mmseq_device_cus() { return device_cus(); }
 
 // Per-call kernel selection (mmseq_gemm `variant`, include/mmseq.h)
 struct GemmSel {

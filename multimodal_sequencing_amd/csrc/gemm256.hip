@@ -113,6 +113,65 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
   st8(reinterpret_cast<us*>(a.C) + off, v);
 }
 
+// MX-fp8 output of one (row block, 32-column half) call: the lane's 8 outputs (bias + activation
+// exactly as epi8, then rounded to bf16 as a bf16 output would be) join the 3 other lanes with the
+// same row (g = 0..3: 32 columns = one E8M0 block) for the block's amax, then quantise like
+// mmseq_quant_mxfp8 (bit-identical to it on the bf16 output): 8 e4m3 bytes per lane, the scale
+// byte by lane group 0; rows in [M, M rounded up to 64) get scale 0, as the quantiser writes.
+template <int ACT>
+__device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, f32x4 lo, f32x4 hi,
+                                        const EpiBias& bias) {
+  float v[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
+    v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
+  }
+  if (ACT == MMSEQ_ACT_GELU_ERF) {
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) {
+      const f32x2 y = gelu_fwd_pair((f32x2){v[r], v[r + 1]});
+      v[r] = y[0];
+      v[r + 1] = y[1];
+    }
+  } else if (ACT) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    v[r] = bf2f(f2bf(v[r]));
+    amax = fmaxf(amax, fabsf(v[r]));
+  }
+  amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  int e = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
+  e = max(-127, min(127, e - 8));
+  const float inv = ldexpf(1.f, -e);
+  const int Mp = (a.M + 63) & ~63;
+  if (g == 0 && m < Mp && n < a.N) {
+    const int KB = a.N >> 5;
+    a.q8_scales[((int64_t)(m >> 6) * KB + (n >> 5)) * 64 + (m & 15) * 4 + ((m >> 4) & 3)] =
+        (uint8_t)(m < a.M ? e + 127 : 0);
+  }
+  if (m >= a.M || n >= a.N) return;
+  uint32_t w[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float s0 = fminf(448.f, fmaxf(-448.f, v[4 * j] * inv));
+    const float s1 = fminf(448.f, fmaxf(-448.f, v[4 * j + 1] * inv));
+    const float s2 = fminf(448.f, fmaxf(-448.f, v[4 * j + 2] * inv));
+    const float s3 = fminf(448.f, fmaxf(-448.f, v[4 * j + 3] * inv));
+    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+    pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+    w[j] = (uint32_t)pk;
+  }
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(a.C) + (int64_t)m * a.ldc + n) =
+      (u32x2){w[0], w[1]};
+}
+
 // ---------------------------------------------------------------------------------------------
 // Large NT kernel (forward / dgrad over the 164k-row activations): persistent 256 x 256 tiles,
 // 8 waves (2 along M x 4 along N, 128 x 64 outputs each = 8 x 4 MFMA 16x16 tiles), BK = 64,
@@ -148,7 +207,7 @@ __device__ __forceinline__ int g8_of(int X, int q) {
   return 4 + (q & 3) + ((q >> 2) << 3);
 }
 
-template <int ACT, bool BWD, bool XIN>
+template <int ACT, bool BWD, bool XIN, bool Q8 = false>  // Q8: MX-fp8 output (epi8_q8)
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles,
                                                             int delay) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF];  // 128 KB
@@ -368,6 +427,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
                                  acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
                                  t ? bias1 : bias0);
       }
+    } else if (Q8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          epi8_q8<ACT>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, g,
+                       acc[i][2 * t], acc[i][2 * t + 1], t ? bias1 : bias0);
     } else {
       const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
 #pragma unroll
@@ -795,6 +861,25 @@ bool mmseq_gemm256_tn(const GemmArgs& a, hipStream_t s, hipError_t* err) {
   const int tn = (a.N + 255) / 256;
   const int ntiles = ((a.M + 255) / 256) * tn;
   hipLaunchKernelGGL(gemm256_tn_kernel, dim3(ntiles * a.splitk), dim3(512), 0, s, a, tn, ntiles);
+  *err = hipGetLastError();
+  return true;
+}
+
+bool mmseq_gemm256_nt_q8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_t* err) {
+  auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  if (a.K % 128 != 0 || a.N % 32 != 0 || a.ldc % 16 != 0 || a.splitk != 1 || !a.q8_scales ||
+      !a16(a.C) || a.resid || a.aux || a.dact || a.accumulate || a.drop.thr)
+    return false;
+  if (a.act != 0 && a.act != MMSEQ_ACT_GELU_ERF && a.act != MMSEQ_ACT_QUICKGELU) return false;
+  const int tn = (a.N + 255) / 256;
+  const int ntiles = ((a.M + 255) / 256) * tn;
+  const dim3 grid(ntiles < num_cu ? ntiles : num_cu), block(512);
+  if (a.act == MMSEQ_ACT_GELU_ERF)
+    hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, false, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
+  else if (a.act == MMSEQ_ACT_QUICKGELU)
+    hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, false, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
+  else
+    hipLaunchKernelGGL((gemm256_nt_kernel<0, false, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
   *err = hipGetLastError();
   return true;
 }

@@ -16,6 +16,7 @@ struct GemmArgs {
   Drop drop;                            // dropout after the activation, before the residual
   float* cs;       // TN wgrad: fused bias gradient cs[m] += sum_k A[k][m] (nullptr: off)
   float* cs_slab;  // ... per-split partials [splitk][M] when splitk > 1
+  uint8_t* q8_scales;  // 256 NT kernel, MX-fp8 output: C is e4m3 [M][ldc] + these packed scales
 };
 
 template <typename TO>
@@ -118,6 +119,12 @@ __device__ __forceinline__ void dma16(rsrc_t r, unsigned short* lds, uint32_t vo
 // delay: shader cycles by which the blocks with one tile fewer start late (0: none)
 bool mmseq_gemm256_nt(const mmseq_gemm_detail::GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s,
                       hipError_t* err, int variant, int delay);
+// ... with the activations written as MX-fp8 (e4m3 + packed E8M0 per 32 columns, fp8.hip
+// layout) instead of bf16: the consumer GEMM's A operand without a quantisation pass
+bool mmseq_gemm256_nt_q8(const mmseq_gemm_detail::GemmArgs& a, int num_cu, hipStream_t s,
+                         hipError_t* err);
+// CU count of the current device (write-once per-device table, gemm.hip)
+int mmseq_device_cus();
 // 256 x 256 TN (wgrad) kernel, fp32 out: a.splitk / a.kchunk (multiple of 128) / a.slab set by the
 // caller (slab [splitk][M][N] when splitk > 1); returns false when its preconditions fail
 bool mmseq_gemm256_tn(const mmseq_gemm_detail::GemmArgs& a, hipStream_t s, hipError_t* err);

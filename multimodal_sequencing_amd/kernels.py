@@ -46,8 +46,11 @@ def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=No
 
 # ------------------------------------------------------------------------------------------------
 # MX-fp8 inference GEMMs (BASELINE config 5): under `fp8_forward()`, the no-grad forward of the
-# encoder layers runs QKV / output / MLP GEMMs as mmseq_quant_mxfp8 (activations, per call) +
-# mmseq_gemm_mxfp8 (weights quantised once per store version). Training keeps bf16.
+# encoder layers runs each MLP as FC1 + activation with an MX-fp8 epilogue (mmseq_gemm_mxfp8_out:
+# the activations leave the GEMM already quantised) and FC2 on the fp8 MFMA (mmseq_gemm_mxfp8, its
+# weight quantised once per store version). QKV and the attention output projection stay bf16: at
+# K = H their fp8 GEMM is no faster than bf16 and a separate activation quantisation pass would be
+# pure cost (profiles/r2s2_fp8_gemm_fastact.json). Training keeps bf16.
 _FP8 = {"on": False, "cache": {}}
 
 
@@ -77,18 +80,18 @@ def _fp8_weight(st, W):
     return hit[2]
 
 
-def _linear_fwd(st, x, W, bias=None, act=0, aux=None, resid=None, drop=None):
-    """_linear, or its MX-fp8 form when enabled and eligible (no dropout, no saved
-    pre-activation, bf16, K % 128 == 0)."""
-    K = x.shape[-1]
-    if (_FP8["on"] and aux is None and drop is None and x.dtype == torch.bfloat16
-            and K % 128 == 0 and x.is_contiguous()):
+def _mlp_fwd(st, x, Wi, bi, act, Wo, bo, resid, lin):
+    """resid + FC2(act(FC1(x))) of a no-grad forward; under fp8_forward() (bf16, K % 128 == 0,
+    FC1 width % 128 == 0) FC1 writes MX-fp8 from its epilogue and FC2 runs on the fp8 MFMA."""
+    K, F = x.shape[-1], Wi.shape[0]
+    if (_FP8["on"] and x.dtype == torch.bfloat16 and K % 128 == 0 and F % 128 == 0
+            and x.is_contiguous() and resid.is_contiguous()):
         R = x.numel() // K
-        out = torch.empty(R, W.shape[0], device=x.device, dtype=x.dtype)
-        N.gemm_mxfp8(N.quant_mxfp8(x.view(R, K)), _fp8_weight(st, W), out, bias=bias, act=act,
-                     resid=None if resid is None else resid.view(R, -1))
+        q = N.gemm_mxfp8_out(x.view(R, K), Wi, bias=bi, act=act)
+        out = torch.empty(R, Wo.shape[0], device=x.device, dtype=x.dtype)
+        N.gemm_mxfp8(q, _fp8_weight(st, Wo), out, bias=bo, resid=resid.view(R, -1))
         return out
-    return _linear(x, W, bias=bias, act=act, aux=aux, resid=resid, drop=drop)
+    return lin(lin(x, Wi, bias=bi, act=act), Wo, bias=bo, resid=resid)
 
 
 def _dgrad(dy, WT, resid=None, act=0, dact=None, out=None):
@@ -160,25 +163,29 @@ class BertLayerFn(torch.autograd.Function):
         d_att, d_o, d_out = drops
         Wqkv = st.packed(L.qkv_w, "w")
         bqkv = st.packed(L.qkv_b, "f32").view(-1)
-        qkv = _linear_fwd(st, x, Wqkv, bias=bqkv) if not save else _linear(x, Wqkv, bias=bqkv)
+        qkv = _linear(x, Wqkv, bias=bqkv)
         o = torch.empty_like(x)
         lse = torch.empty(P, heads, T, device=x.device)
         # the forward's dropout keep mask as bits (1 bit per score; read back by the backward)
         kbits = (N.attn_keep_bits(P, T, heads, x.device) if d_att is not None and save else None)
         N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
                    H, lse, drop=d_att, keep_bits=kbits)
-        s1 = (_linear_fwd(st, o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, drop=d_o) if not save
-              else _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, drop=d_o))
+        s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, drop=d_o)
         h1 = torch.empty_like(x)
         m1 = torch.empty(s1.shape[0], device=x.device)
         r1 = torch.empty_like(m1)
         N.layernorm_fwd(s1.shape[0], H, s1, _rows(H), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, h1,
                         _rows(H), m1, r1)
-        z = (torch.empty(x.shape[0], st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype)
-             if save else None)
-        lin = _linear if save else (lambda *a, **k: _linear_fwd(st, *a, **k))
-        gact = lin(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU, aux=z)
-        s2 = lin(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1, drop=d_out)
+        if save:
+            z = torch.empty(x.shape[0], st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype)
+            gact = _linear(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU, aux=z)
+            s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1, drop=d_out)
+        elif d_out is None:
+            s2 = _mlp_fwd(st, h1, st.w(L.i_w), st.f32(L.i_b), GELU, st.w(L.out_w),
+                          st.f32(L.out_b), h1, _linear)
+        else:
+            gact = _linear(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU)
+            s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1, drop=d_out)
         y = torch.empty_like(x)
         m2 = torch.empty_like(m1)
         r2 = torch.empty_like(m1)
@@ -246,23 +253,23 @@ class VitBlockFn(torch.autograd.Function):
         hn = torch.empty_like(h)
         N.layernorm_fwd(R, W, h, _rows(W), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, hn, _rows(W),
                         m1, r1)
-        lin = _linear if save else (lambda *a, **k: _linear_fwd(st, *a, **k))
-        qkv = lin(hn, st.w(L.in_w), bias=st.f32(L.in_b))
+        qkv = _linear(hn, st.w(L.in_w), bias=st.f32(L.in_b))
         o = torch.empty_like(h)
         lse = torch.empty(P, heads, T, device=h.device)
         N.attn_fwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
                    lse)
-        x1 = lin(o, st.w(L.out_w), bias=st.f32(L.out_b), resid=h)
+        x1 = _linear(o, st.w(L.out_w), bias=st.f32(L.out_b), resid=h)
         m2 = torch.empty_like(m1)
         r2 = torch.empty_like(m1)
         hn2 = torch.empty_like(h)
         N.layernorm_fwd(R, W, x1, _rows(W), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, hn2, _rows(W),
                         m2, r2)
-        z = torch.empty(R, st.w(L.fc_w).shape[0], device=h.device, dtype=h.dtype) if save else None
-        gact = lin(hn2, st.w(L.fc_w), bias=st.f32(L.fc_b), act=QGELU, aux=z)
-        x2 = lin(gact, st.w(L.proj_w), bias=st.f32(L.proj_b), resid=x1)
         if not save:
-            return x2
+            return _mlp_fwd(st, hn2, st.w(L.fc_w), st.f32(L.fc_b), QGELU, st.w(L.proj_w),
+                            st.f32(L.proj_b), x1, _linear)
+        z = torch.empty(R, st.w(L.fc_w).shape[0], device=h.device, dtype=h.dtype)
+        gact = _linear(hn2, st.w(L.fc_w), bias=st.f32(L.fc_b), act=QGELU, aux=z)
+        x2 = _linear(gact, st.w(L.proj_w), bias=st.f32(L.proj_b), resid=x1)
         ctx.save_for_backward(h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact)
         ctx.meta = (L, P, T, heads)
         return x2

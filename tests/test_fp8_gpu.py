@@ -136,3 +136,26 @@ def test_gemm_epilogue_bias_gelu_resid():
     ref = torch.nn.functional.gelu(pre) + resid.double()
     err = (C.double() - ref).abs() / (ref.abs() + 1.0)
     assert float(err.max()) < 1e-2, float(err.max())
+
+
+@pytest.mark.parametrize("rows,Nn,K,act", [(300, 320, 256, 1), (1000, 4096, 1024, 1),
+                                           (257, 64, 128, 0), (65, 512, 384, 2)])
+def test_gemm_mxfp8_out_matches_gemm_then_quant(rows, Nn, K, act):
+    """MX-fp8 written by the GEMM epilogue (mmseq_gemm_mxfp8_out) is bit-identical to the bf16
+    GEMM output (same activation) quantised by mmseq_quant_mxfp8: codes, and the packed scales
+    including the zero rows up to the next multiple of 64."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows * 7 + Nn + K)
+    x = torch.randn(rows, K, device=DEV, generator=g).bfloat16()
+    W = (torch.randn(Nn, K, device=DEV, generator=g) * 0.05).bfloat16()
+    b = torch.randn(Nn, device=DEV, generator=g) * 0.1
+    ref = torch.empty(rows, Nn, device=DEV, dtype=torch.bfloat16)
+    N.gemm_set_fast(4)  # the 256 x 256 kernel: the same epilogue arithmetic
+    try:
+        N.gemm(x, W, ref, rows, Nn, K, bias=b, act=act)
+    finally:
+        N.gemm_set_fast(1)
+    want = N.quant_mxfp8(ref)
+    got = N.gemm_mxfp8_out(x, W, bias=b, act=act)
+    assert torch.equal(got.q[:, :Nn], want.q[:, :Nn])
+    assert torch.equal(got.scales, want.scales)

@@ -334,7 +334,7 @@ def test_config5_shape_fp8_forward_close_to_reference():
         base = m(inputs)[0].item()
         with K.fp8_forward():
             loss = m(inputs)[0].item()
-            assert len(K._FP8["cache"]) >= 8  # 2 ViT blocks + 2 joint layers x 4 weights
+            assert len(K._FP8["cache"]) >= 4  # the FC2 weight of 2 ViT blocks + 2 joint layers
     ref = float(d["loss"])
     assert abs(loss - ref) < 5e-2 * abs(ref), (loss, base, ref)
     assert abs(loss - base) < 5e-2 * abs(ref), (loss, base)

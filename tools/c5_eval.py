@@ -1,0 +1,29 @@
+"""Config-5 eval forward only (no grad), one mode per process, for per-kernel comparison of the
+bf16 and MX-fp8 encoder GEMMs under rocprofv3 --kernel-trace --stats:
+    python tools/c5_eval.py bf16|mxfp8 [iters]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from multimodal_sequencing_amd import kernels as K, model_zoo  # noqa: E402
+
+mode = sys.argv[1]
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+dev = torch.device("cuda:0")
+preset = model_zoo.PRESETS["config5"]
+m = model_zoo.build_preset("config5", device=dev, dtype=torch.bfloat16, seed=0).eval()
+data = bench.synthetic_batch(1, preset["N"], preset["per_seq"], 50265, 224, dev, seed=3000)
+with torch.no_grad(), K.fp8_forward(mode == "mxfp8"):
+    for _ in range(2):
+        m(data)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        lv = m(data)[0]
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+print(f'{{"mode": "{mode}", "ms_per_story": {dt * 1e3:.2f}, "loss": {float(lv):.6f}}}')
