@@ -148,6 +148,114 @@ __global__ __launch_bounds__(256, 2) void gemm_mxfp8_nt_kernel(GemmArgs a, const
     }
 }
 
+template <int ROWS_PER_WAVE>  // rows of 128 B one wave stages: 8 per DMA instruction
+__device__ __forceinline__ void stage_rows(rsrc_t r, int64_t ld, int k0, uint8_t* s, int wave,
+                                           int lane) {
+  constexpr int NI = ROWS_PER_WAVE / 8;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int inst = wave * NI + i;
+    const int row = inst * 8 + (lane >> 3), cp = lane & 7;
+    dma_chunk(r, s + inst * 1024, (uint32_t)((int64_t)row * ld + k0 + ((cp ^ (row & 7)) << 4)));
+  }
+}
+
+// 256 x 256 tiles, 8 waves (4 x 2, 64 x 128 each), BK = 128, 2-slot LDS-DMA ring (2 x 66 KB).
+// The main loop is bound by the latency of the operand DMA (PMC at the config-5 FC2 shape: MFMA
+// busy 0.39, 43 % of wave time in memory waits, L2 hit 79 %): the bytes a CU can keep in flight
+// are what LDS leaves beside the slot being computed, so the rate per CU goes with MFLOP per
+// staged byte. 256 x 256 stages half the bytes per MFLOP of 128 x 128 (1.13x at FC2, 1.08x at
+// QKV); a 256 x 128 tile with a 3-slot ring and register-double-buffered fragments measured no
+// better than 128 x 128 (same bytes in flight per MFLOP). The B fragments of a step are read in
+// two halves of four 16-column blocks to stay inside the register file (128 accumulators).
+constexpr int kQ_A = 256 * 128, kQ_B = 256 * 128;
+constexpr int kQSlot = kQ_A + kQ_B + 1024 + 1024;
+
+__global__ __launch_bounds__(512, 1) void gemm_mxfp8_nt256x256_kernel(GemmArgs a, const uint8_t* sa,
+                                                                     const uint8_t* sb,
+                                                                     int64_t sa_bytes,
+                                                                     int64_t sb_bytes, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kQSlot];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int Lr = xcd_item(blockIdx.x, gridDim.x);
+  const int tm = Lr / tiles_n, tn = Lr % tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(a.A);
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(a.B);
+  const int KB = a.K / 32, nk = a.K / 128;
+  const rsrc_t ra = make_rsrc(A + (int64_t)m0 * a.lda, (int64_t)(a.M - m0 - 1) * a.lda + a.K);
+  const rsrc_t rb = make_rsrc(B + (int64_t)n0 * a.ldb, (int64_t)(a.N - n0 - 1) * a.ldb + a.K);
+  const rsrc_t rsa = make_rsrc(sa, sa_bytes), rsb = make_rsrc(sb, sb_bytes);
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // per wave and step: 4 A + 4 B DMA instructions and one for the scales (waves 0-3 one A row
+  // group of 64 rows each, waves 4-7 one B row group each; 16 lanes x 16 B)
+  auto issue = [&](int kt) {
+    uint8_t* s = smem + (kt & 1) * kQSlot;
+    stage_rows<32>(ra, a.lda, kt * 128, s, wave, lane);
+    stage_rows<32>(rb, a.ldb, kt * 128, s + kQ_A, wave, lane);
+    if (lane < 16) {
+      const bool isa = wave < 4;  // wave-uniform
+      const int grp = ((isa ? m0 : n0) >> 6) + (wave & 3);
+      dma_chunk(isa ? rsa : rsb, s + kQ_A + kQ_B + wave * 256,
+                (uint32_t)(((int64_t)grp * KB + 4 * kt) * 64 + lane * 16));
+    }
+  };
+
+  issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's DMA of step kt retired and its reads of the other slot (step kt - 1) too; after
+    // the barrier that slot takes the DMA of step kt + 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) issue(kt + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint8_t* s = smem + (kt & 1) * kQSlot;
+    const int so = (lane >> 4) * 64 + (lane & 15) * 4;
+    const int scA = *reinterpret_cast<const int*>(s + kQ_A + kQ_B + wr * 256 + so);
+    i32x8 fa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag(s, wr * 64 + i * 16, lane);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int scB = *reinterpret_cast<const int*>(s + kQ_A + kQ_B + 1024 + (wc * 2 + h) * 256 + so);
+      i32x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag(s + kQ_A, wc * 128 + h * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][h * 4 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              fb[j], fa[i], acc[i][h * 4 + j], 0, 0, 0, (int)((uint32_t)scB >> (8 * j)), 0,
+              (int)((uint32_t)scA >> (8 * i)));
+    }
+  }
+
+  const int g = lane >> 4, ii = lane & 15;
+  unsigned short* C = reinterpret_cast<unsigned short*>(a.C);
+  const unsigned short* resid = reinterpret_cast<const unsigned short*>(a.resid);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + wr * 64 + i * 16 + ii;
+      const int n = n0 + wc * 128 + j * 16 + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epilogue4<unsigned short>(a, C, resid, nullptr, nullptr, m, n, v);
+    }
+}
+
 // bf16 / f32 [M][K] -> e4m3 [M][K] (row stride ldq) + packed E8M0 scales; one thread per
 // (row, 32-element block), rows up to the next multiple of 64 get scale 0
 template <typename TI>
@@ -239,14 +347,18 @@ extern "C" mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int
   MMSEQ_REQUIRE(((uintptr_t)C & 7) == 0 && (!resid || ((uintptr_t)resid & 7) == 0),
                 "gemm_mxfp8: 8-byte aligned output");
   if (M == 0) return MMSEQ_OK;
-  const int tiles_m = (M + 127) / 128, tiles_n = (N + 127) / 128;
+  // 256 x 256 tiles once there are rows and columns for them, else 128 x 128
+  const bool wide = M >= 512 && N >= 256;
+  const int tile = wide ? 256 : 128;
+  const int tiles_m = (M + tile - 1) / tile, tiles_n = (N + tile - 1) / tile;
   MMSEQ_REQUIRE((int64_t)tiles_m * tiles_n < (1ll << 31), "gemm_mxfp8: too many tiles");
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K;
   a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
   a.bias = bias; a.act = act; a.resid = resid; a.ldr = ldr; a.alpha = alpha;
   a.vec_c = 1;
-  hipLaunchKernelGGL(gemm_mxfp8_nt_kernel, dim3(tiles_m * tiles_n), dim3(256), 0,
+  hipLaunchKernelGGL(wide ? gemm_mxfp8_nt256x256_kernel : gemm_mxfp8_nt_kernel,
+                     dim3(tiles_m * tiles_n), dim3(wide ? 512 : 256), 0,
                      reinterpret_cast<hipStream_t>(stream), a, (const uint8_t*)a_scales,
                      (const uint8_t*)b_scales, mmseq_mxfp8_scale_bytes(M, K),
                      mmseq_mxfp8_scale_bytes(N, K), tiles_n);

@@ -144,8 +144,15 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
     v[r] = bf2f(f2bf(v[r]));
     amax = fmaxf(amax, fabsf(v[r]));
   }
-  amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  // max over lanes l ^ 16 and l ^ 32 with the gfx950 row swaps (no LDS round trip as with
+  // ds_bpermute); amax >= 0, so its bit pattern orders like the value
+  {
+    uint32_t u = __float_as_uint(amax);
+    const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    u = max(r16[0], r16[1]);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    amax = __uint_as_float(max(r32[0], r32[1]));
+  }
   int e = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
   e = max(-127, min(127, e - 8));
   const float inv = ldexpf(1.f, -e);

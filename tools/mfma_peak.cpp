@@ -13,6 +13,7 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 template <int SHAPE>
 __global__ void __launch_bounds__(256) mfma_loop(const unsigned short* __restrict__ seed, int iters,
@@ -27,7 +28,22 @@ __global__ void __launch_bounds__(256) mfma_loop(const unsigned short* __restric
     b[j] = __builtin_bit_cast(__bf16, v);
   }
   float out = 0.f;
-  if constexpr (SHAPE == 16) {
+  if constexpr (SHAPE == 8) {
+    i32x8 fa, fb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // e4m3 bytes with the exponent's top bit clear: finite, no NaN
+      fa[j] = (int)((((uint32_t)a[j % 8] << 16) | (uint32_t)b[j % 8]) & 0x37373737u);
+      fb[j] = (int)((((uint32_t)b[j % 8] << 16) | (uint32_t)a[(j + 3) % 8]) & 0x37373737u);
+    }
+    f32x4 acc[8] = {};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        acc[k] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa, fb, acc[k], 0, 0, 0, 127, 0, 127);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+  } else if constexpr (SHAPE == 16) {
     f32x4 acc[8] = {};
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
@@ -78,8 +94,8 @@ static double run(int cus, int iters) {
   hipEventSynchronize(e1);
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
-  const double per_mfma = SHAPE == 16 ? 2.0 * 16 * 16 * 32 : 2.0 * 32 * 32 * 16;
-  const double per_wave_iter = SHAPE == 16 ? 8 : 4;
+  const double per_mfma = SHAPE == 8 ? 2.0 * 16 * 16 * 128 : SHAPE == 16 ? 2.0 * 16 * 16 * 32 : 2.0 * 32 * 32 * 16;
+  const double per_wave_iter = SHAPE == 32 ? 4 : 8;
   const double flops = (double)reps * blocks * 4 * iters * per_wave_iter * per_mfma;
   hipFree(d);
   hipFree(sink);
@@ -94,8 +110,10 @@ int main() {
   const int iters = 40000;
   double t16 = run<16>(cus, iters);
   double t32 = run<32>(cus, iters);
+  double t8 = run<8>(cus, iters / 2);
   printf("{\"device\": \"%s\", \"cus\": %d, \"iters_per_wave\": %d, \"bf16_16x16x32_tflops\": %.1f, "
-         "\"bf16_32x32x16_tflops\": %.1f, \"spec_dense_bf16_tflops\": 2500.0, \"operands\": \"random bf16 in registers\"}\n",
-         p.gcnArchName, cus, iters, t16, t32);
+         "\"bf16_32x32x16_tflops\": %.1f, \"mxfp8_16x16x128_tflops\": %.1f, \"spec_dense_bf16_tflops\": 2500.0, "
+         "\"spec_dense_fp8_tflops\": 5000.0, \"operands\": \"random bf16 / e4m3 in registers\"}\n",
+         p.gcnArchName, cus, iters, t16, t32, t8);
   return 0;
 }
