@@ -87,7 +87,8 @@ def _exact_operand(g, rows, K):
     return (v.view(rows, K // 32, 32) * torch.pow(2.0, e)[..., None]).view(rows, K)
 
 
-@pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 256, 512), (1000, 384, 1024)])
+@pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 256, 512), (1000, 384, 1024),
+                                   (700, 640, 128)])  # last two: 256^2 tiles, ragged M and N
 def test_gemm_exact_operands(M, N, K):
     from multimodal_sequencing_amd import _native as N_
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
@@ -121,10 +122,10 @@ def test_gemm_random_tolerance(M, N, K):
     assert rel < 6e-2, rel  # the stated MX-fp8 tolerance vs the unquantised product
 
 
-def test_gemm_epilogue_bias_gelu_resid():
+@pytest.mark.parametrize("M,N,K", [(300, 256, 256), (600, 320, 384)])  # 128^2 / 256^2 kernel
+def test_gemm_epilogue_bias_gelu_resid(M, N, K):
     from multimodal_sequencing_amd import _native as N_
     g = torch.Generator(device=DEV).manual_seed(3)
-    M, N, K = 300, 256, 256
     A = _exact_operand(g, M, K) / 64
     B = _exact_operand(g, N, K) / 64
     bias = torch.randn(N, device=DEV, generator=g)
