@@ -91,10 +91,13 @@ class BertForOrdering(nn.Module):
                                             getattr(config, "initializer_range", 0.02)),
                                 device, torch.float32)
         self.store.init_weights(seed=seed)
+        # the inner model's slot comes first, as in the reference (`self.bert` is set before the
+        # head at modeling_bert.py:860-866): named_parameters() order is what a reference-written
+        # optimizer.pt indexes by position (trainer.FusedAdamW.load_state_dict)
+        self.add_module("bert", inner_model)
         attach_tree(self, self.store.params)
         self._anchor = torch.zeros((), device=device, requires_grad=True)
         self.device_ = torch.device(device)
-        self.bert = inner_model
         self._maps = {}
         self.hidden_dropout_prob = getattr(config, "hidden_dropout_prob", 0.1)  # :677
         self.para_dropout = getattr(args, "para_dropout", 0.1)  # train.py:2014, :881

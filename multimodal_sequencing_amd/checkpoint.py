@@ -227,7 +227,8 @@ def _resolve_dir(path):
                 ar.extractall(tmp, filter="data")
             except TypeError:  # interpreter without extraction filters
                 for m in ar.getmembers():
-                    if m.name.startswith(("/", "..")) or ".." in m.name.split("/"):
+                    if m.name.startswith(("/", "..")) or ".." in m.name.split("/") or \
+                            m.issym() or m.islnk() or not (m.isfile() or m.isdir()):
                         raise ValueError(f"unsafe member {m.name!r} in {path}")
                 ar.extractall(tmp)
         return tmp, tmp
@@ -293,6 +294,9 @@ def berson_from_pretrained(cls, pretrained_model_name_or_path, *model_args, **kw
         prefix = base + "."
     if hasattr(model, base) and not any(k.startswith(base) for k in state_dict):
         target = getattr(model, base)
+        if target is None:  # the reference would build a BertModel here (modeling_bert.py:860-866)
+            raise ValueError(f"state dict has no '{base}.' keys and the model has no inner "
+                             f"'{base}' module to load them into: pass inner_model=")
     info = load_into(target, state_dict, prefix)
     model.eval()
     model.loading_info = info

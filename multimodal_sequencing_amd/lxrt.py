@@ -152,7 +152,8 @@ class LXRTModel(nn.Module):
                             img_part=multimodal_img_part)
         self.store = ParamStore(specs, device, compute_dtype)
         self.store.init_weights(seed=kw.get("seed", 0))
-        attach_tree(self, self.store.params)
+        from .resnet import rn50_attach_order
+        attach_tree(self, self.store.params, order=rn50_attach_order)
         self._anchor = torch.zeros((), device=device, requires_grad=True)
         self.rn50 = None
         if not multimodal_text_part and self.vision.get("type") == "rn50":

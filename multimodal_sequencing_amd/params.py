@@ -223,10 +223,14 @@ def uniform(bound):
     return lambda g, shape: (torch.rand(shape, generator=g) * 2 - 1) * bound
 
 
-def attach_tree(root: nn.Module, params):
+def attach_tree(root: nn.Module, params, order=None):
     """Register each named nn.Parameter under nested container modules so that
-    root.state_dict() / named_parameters() reproduce the reference's dotted key names."""
-    for name, p in params.items():
+    root.state_dict() / named_parameters() reproduce the reference's dotted key names. `order`
+    (names -> names) sets the registration order where the reference's module order differs
+    from the buffer layout (the submodules are created in first-seen order)."""
+    names = list(params) if order is None else order(list(params))
+    for name in names:
+        p = params[name]
         parts = name.split(".")
         mod = root
         for part in parts[:-1]:

@@ -97,7 +97,11 @@ class LXRTPretraining(nn.Module):
                                                      config.initializer_range, num_answers),
                                 device, compute_dtype)
         self.store.init_weights(seed=seed + 7)
-        attach_tree(self, self.store.params)
+        # the reference builds the MRM head before BertPreTrainingHeads (lxrt/modeling.py:1713,
+        # 1724-1728): registration order = named_parameters() order
+        mrm = "patch_based_mrm_classification_head."
+        attach_tree(self, self.store.params, order=lambda names: (
+            [n for n in names if n.startswith(mrm)] + [n for n in names if not n.startswith(mrm)]))
         # tied LM decoder (:1164-1167): the word table registered under both names
         attach_tree(self, {"cls.predictions.decoder.weight":
                            self.bert.store.params["embeddings.word_embeddings.weight"]})
@@ -180,7 +184,8 @@ class LXRTPretraining(nn.Module):
         D = inner.new_dropouts()
         ph = self.config.hidden_dropout_prob
         # CLIP ViT over the two sub-sampled images of each story (img_len = 2)
-        vout, Tv = inner.visual_forward(images, sub_idx)  # [B * Tv, E]
+        with torch.no_grad():  # only vout.detach() is used: the blocks skip their saves
+            vout, Tv = inner.visual_forward(images, sub_idx)  # [B * Tv, E]
         E = vout.shape[-1]
         # MRM masking (:948-1009): targets = visn_fc(features at the masked patches), the
         # sequence fed on has them zeroed; the ViT's gradient is exactly zero (docstring)

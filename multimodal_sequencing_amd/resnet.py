@@ -96,6 +96,17 @@ def rn50_specs(prefix, layers=(3, 4, 6, 3), width=64, embed=1024, res=224, std=0
     return sp
 
 
+def rn50_attach_order(names):
+    """Registration order of the reference's modules: AttentionPool2d creates k_proj before
+    q_proj (clip/model.py:60-64), while the packed QKV operand keeps q | k | v in the buffer."""
+    k = [n for n in names if ".attnpool.k_proj." in n]
+    if not k:
+        return names
+    rest = [n for n in names if n not in set(k)]
+    i = next(j for j, n in enumerate(rest) if ".attnpool.q_proj." in n)
+    return rest[:i] + k + rest[i:]
+
+
 def rn50_buffer_names(prefix, layers=(3, 4, 6, 3), width=64):
     """{bn module name: channels} of every BatchNorm (running stats are buffers)."""
     stem, blocks = rn50_arch(layers, width)

@@ -256,6 +256,51 @@ def test_optimizer_scheduler_resume(tmp_path):
     _same_moments(m, opt, opt3)
 
 
+@pytest.mark.parametrize("name", ["tiny", "tiny_textonly", "rn50_eval"])
+def test_parameter_order_is_the_references(name):
+    """named_parameters() runs in the reference's module order (modeling_bert.py:860-866 sets
+    `self.bert` before the head; AttentionPool2d creates k_proj before q_proj, clip/model.py:
+    60-64). The fixture's `shapes` were written from the reference's state_dict() in order."""
+    meta, _, _ = load_fixture(name)
+    m = model_zoo.build_from_golden(meta["config"], device="cpu")
+    ours = [n for n, _ in m.named_parameters()]
+    ref = [k for k in meta["shapes"] if k in set(ours)]
+    assert len(ref) == len(ours) and ref == ours
+
+
+def test_positional_optimizer_state_from_reference_order():
+    """A reference-written optimizer.pt carries no names: train.py:172-183 builds the decay and
+    no-decay groups from model.named_parameters() in the REFERENCE's order, and AdamW numbers
+    the parameters 0.. across the groups. Each moment here encodes its parameter's identity, so
+    a wrong positional match shows up as a wrong value (or a numel mismatch)."""
+    meta, m, params = _tiny()
+    ref_names = list(meta["shapes"])
+    no_decay = ("bias", "LayerNorm.weight")
+    groups = [[n for n in ref_names if not any(nd in n for nd in no_decay)],
+              [n for n in ref_names if any(nd in n for nd in no_decay)]]
+    state, pg, idx = {}, [], 0
+    for gi, names in enumerate(groups):
+        ids = []
+        for n in names:
+            shape = tuple(meta["shapes"][n])
+            state[idx] = {"step": 3, "exp_avg": torch.full(shape, float(idx)),
+                          "exp_avg_sq": torch.full(shape, float(idx) + 0.5)}
+            ids.append(idx)
+            idx += 1
+        pg.append({"lr": 1e-5, "betas": (0.9, 0.999), "eps": 1e-8,
+                   "weight_decay": 0.01 if gi == 0 else 0.0, "correct_bias": True, "params": ids})
+    opt = FusedAdamW(m.stores(), lr=1e-5)
+    opt.load_state_dict(m, {"state": state, "param_groups": pg})
+    assert opt.step_count == 3
+    pos = {n: i for i, n in enumerate(groups[0] + groups[1])}
+    for i, s in enumerate(m.stores()):
+        for sname, p in s.params.items():
+            full = next(n for n, q in m.named_parameters() if q is p)
+            o, k = s.offsets[sname], p.numel()
+            assert torch.all(opt.m[i][o:o + k] == pos[full]), full
+            assert torch.all(opt.v[i][o:o + k] == pos[full] + 0.5), full
+
+
 def _same_moments(m, a, b):
     """every parameter's span round-trips (alignment padding is not state)"""
     for i, s in enumerate(m.stores()):

@@ -57,6 +57,15 @@ def test_pretrain_state_dict_matches_reference():
         sd["bert.embeddings.word_embeddings.weight"].data_ptr()  # tied (:1164-1167)
 
 
+def test_pretrain_parameter_order_is_the_references():
+    """named_parameters() order equals the reference's (the MRM head is built before
+    BertPreTrainingHeads, lxrt/modeling.py:1713,1724-1728): positional optimizer.pt resume."""
+    meta, _ = _load()
+    m = _build(meta, "cpu", torch.float32)
+    ours = [n for n, _ in m.named_parameters()]
+    assert [k for k in meta["shapes"] if k in set(ours)] == ours
+
+
 def test_pretrain_draw_structure():
     meta, d = _load()
     m = _build(meta, "cpu", torch.float32)
