@@ -5,6 +5,12 @@ mode "overlap": the product model's real grad layout (tiny golden config on CPU)
                 backward writes each unit's gradient and reports it in backward order, exactly
                 as the layer Functions do, with the reducer armed; buckets must be issued
                 during the "backward" and the result must equal one flat all-reduce.
+mode "real":    GPU (every rank on cuda:0, gloo): the product model (fp32, eval) under a REAL
+                loss.backward() with the reducer armed; one story per rank. Every bucket's
+                chunk is snapshotted at the moment it is issued and compared with the rank's
+                final local gradient from an unarmed backward of the same story (a bucket that
+                fired before its gradients were final differs); rank 0 also runs the
+                single-process step over all the ranks' stories for the parent to compare.
 """
 import json
 import os
@@ -75,11 +81,106 @@ def overlap(out, rank):
                    "buckets": [len(red.plan[id(s)]["buckets"]) for s in stores]}, f)
 
 
+REAL_CFG = {"B": 2, "N": 5, "per_seq": 8, "ragged": False, "text_only": False,
+            "vit": {"embed": 96, "res": 32, "layers": 5, "width": 128, "patch": 8},
+            "joint": {"vocab": 300, "hidden": 128, "layers": 6, "heads": 2, "inter": 512,
+                      "max_pos": 514},
+            "head": {"ff": 256, "heads": 8, "layers": 2}}
+
+
+def real_inputs(world, seed=7):
+    """`world` equal-length stories (make_golden.make_inputs layout), one per rank."""
+    import numpy as np
+    c = REAL_CFG
+    g = np.random.RandomState(seed)
+    B, N, k = world, c["N"], c["per_seq"] - 2
+    ids = np.ones((B, N * c["per_seq"]), dtype=np.int64)
+    for b in range(B):
+        ids[b] = np.concatenate([[0] + list(g.randint(3, c["joint"]["vocab"], size=k)) + [2]
+                                 for _ in range(N)])
+    labels = np.stack([np.argsort(g.permutation(N)) for _ in range(B)]).astype(np.int64)
+    R = c["vit"]["res"]
+    images = g.standard_normal((B, N, 3, R, R)).astype(np.float32)
+    return {"input_ids": torch.from_numpy(ids), "labels": torch.from_numpy(labels),
+            "images": torch.from_numpy(images)}
+
+
+def real(out, rank):
+    from multimodal_sequencing_amd import model_zoo
+    world = dist.get_world_size()
+    dev = "cuda:0"  # every rank shares the box's one GPU
+    m = model_zoo.build_from_golden(REAL_CFG, device=dev)
+    m.eval()
+    stores = m.stores()
+    allin = real_inputs(world)
+    mine = {k: v[rank:rank + 1] for k, v in allin.items()}
+    # (1) unarmed backward of this rank's story: the final local gradient
+    local = None
+    for rep in range(2):  # twice: the unarmed backward must itself be bitwise reproducible
+        m.zero_grad()
+        m(mine)[0].backward()
+        torch.cuda.synchronize()
+        again = [s.grad.clone() for s in stores]
+        if local is None:
+            local = again
+    nondet = [(i, float((a - b).abs().max()), float(a.abs().max()))
+              for i, (a, b) in enumerate(zip(local, again)) if not torch.equal(a, b)]
+    # (2) the same backward with the reducer armed; snapshot each chunk when it is issued
+    units, begin = m.ddp_units()
+    red = GradAllReduce(stores, bucket_mb=0.05, units=units, begin_units=begin)
+    snaps, phase = [], ["backward"]
+    fire = red._fire
+
+    def spy(store, j):
+        pl = red.plan[id(store)]
+        if not pl["fired"][j]:
+            lo, hi = pl["buckets"][j][:2]
+            snaps.append((stores.index(store), lo, hi, store.grad[lo:hi].clone(), phase[0]))
+        fire(store, j)
+
+    red._fire = spy
+    m.zero_grad()
+    red.arm(True)
+    loss = m(mine)[0]
+    loss.backward()
+    in_backward = len(red.works)
+    phase[0] = "finish"
+    red.finish()
+    torch.cuda.synchronize()
+    # the embedding-table and pointer-head backward kernels accumulate with float atomics, so
+    # two backwards agree to rounding, not bitwise (`nondeterministic`); a bucket issued before
+    # its gradients were final would miss whole contributions (differences at gradient scale)
+    bad = []
+    for i, lo, hi, snap, _ in snaps:
+        ref = local[i][lo:hi]
+        err = float((snap - ref).abs().max())
+        if err > 1e-5 * float(ref.abs().max()) + 1e-12:
+            bad.append((i, lo, hi, err, float(ref.abs().max())))
+    total = sum(len(red.plan[id(s)]["buckets"]) for s in stores)
+    res = {"fired_in_backward": in_backward, "buckets": total, "snapshots": len(snaps),
+           "early": bad, "loss": float(loss.detach()), "nondeterministic": nondet,
+           "fired": [(i, lo, hi, ph) for i, lo, hi, _, ph in snaps],
+           "unit_buckets_in_finish": sum(1 for i, lo, hi, _, ph in snaps if ph == "finish" and
+                                         any(b[:2] == [lo, hi] and b[2] for b in
+                                             red.plan[id(stores[i])]["buckets"]))}
+    torch.save({"grad": [s.grad.cpu() for s in stores], "local": [x.cpu() for x in local]},
+               os.path.join(out, f"real{rank}.pt"))
+    if rank == 0:  # (3) one process, all stories in one batch (the DP mean's target)
+        m.zero_grad()
+        full = m(allin)[0]
+        full.backward()
+        torch.cuda.synchronize()
+        torch.save([s.grad.cpu() for s in stores], os.path.join(out, "single.pt"))
+        res["single_loss"] = float(full)
+    with open(os.path.join(out, f"real{rank}.json"), "w") as f:
+        json.dump(res, f)
+
+
 def main():
     out, mode = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "flat")
     dist.init_process_group("gloo")
     rank = dist.get_rank()
-    {"flat": flat, "overlap": overlap}[mode](out, rank)
+    {"flat": flat, "overlap": overlap, "real": real}[mode](out, rank)
     dist.destroy_process_group()
 
 

@@ -20,9 +20,12 @@ from multimodal_sequencing_amd.lxrt import LXRTConfig
 from multimodal_sequencing_amd.pretraining import LXRTPretraining
 
 
-def _load():
-    meta = json.load(open(os.path.join(GOLDEN, "pretrain_tiny.json")))
-    d = dict(np.load(os.path.join(GOLDEN, "pretrain_tiny.npz")))
+def _load(name="pretrain_tiny"):
+    meta = json.load(open(os.path.join(GOLDEN, f"{name}.json")))
+    d = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
+    if "input_ids" not in d:  # real-shape fixture: inputs regenerated from the seed
+        from make_golden_pretrain import pretrain_inputs
+        d["input_ids"], d["images"] = pretrain_inputs(meta["config"], meta["seed"] + 1)
     return meta, d
 
 
@@ -84,8 +87,8 @@ def test_pretrain_draw_structure():
     assert d["mask_idx"].shape == (meta["config"]["B"], 10)
 
 
-def _run(dtype):
-    meta, d = _load()
+def _run(dtype, name="pretrain_tiny"):
+    meta, d = _load(name)
     m = _build(meta, "cuda", dtype)
     m.eval()
     m.zero_grad()
@@ -138,3 +141,78 @@ def test_pretrain_bf16_close_to_reference():
         b = grads[k[3:]].detach().cpu().double().flatten()
         cos = float(a @ b / (a.norm() * b.norm() + 1e-30))
         assert cos > 0.98, (k, cos)
+
+
+# ---- config 2 at its stated size (tests/golden/pretrain_real: ViT-B/16 at 224^2, H = 768,
+# bert-base-uncased vocab 30522, B = 2 stories; reference outputs only, see the generator) ------
+def _sample_check(d, grads, fp32):
+    """Per-parameter gradient norm and the 2 x 1024 recorded samples (make_golden_real.grad_samples)."""
+    from make_golden_real import grad_samples
+    checked = 0
+    for k in d:
+        if not k.startswith("gn::"):
+            continue
+        name = k[4:]
+        if name == "cls.predictions.decoder.weight":
+            continue  # tied: the word table is listed once
+        ref_n = float(d[k])
+        g = grads[name].detach().float().cpu().numpy()
+        h, s = grad_samples(g)
+        if ref_n < 1e-6 * float(d["grad_norm"]):  # exactly or analytically zero (a softmax-CE
+            # shared bias): rounding noise on both sides
+            assert float(np.linalg.norm(g)) < 1e-4 * float(d["grad_norm"]), name
+            checked += 1
+            continue
+        if fp32:
+            assert abs(float(np.linalg.norm(g.astype(np.float64))) - ref_n) < 2e-3 * ref_n, name
+            np.testing.assert_allclose(h, d["gh::" + name], rtol=2e-3, atol=1e-6, err_msg=name)
+            np.testing.assert_allclose(s, d["gs::" + name], rtol=2e-3, atol=1e-6, err_msg=name)
+        else:
+            a = np.concatenate([d["gh::" + name], d["gs::" + name]]).astype(np.float64)
+            b = np.concatenate([h, s]).astype(np.float64)
+            if np.linalg.norm(a) > 1e-3 * ref_n * np.sqrt(a.size / g.size):
+                cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
+                assert cos > 0.98, (name, cos)
+        checked += 1
+    assert checked > 20
+    return checked
+
+
+@pytest.mark.gpu
+def test_pretrain_real_shape_fp32_matches_reference():
+    """Config 2 at its real shape, fp32 parity mode: total loss 1e-4, the heads, and the LM head
+    over all 393 visual tokens to 30522 words — the padded-ldc MFMA GEMM (pretraining.py) — full
+    rows and the logsumexp of every row; per-parameter gradient norms and samples."""
+    meta, d, m, loss, losses, answer = _run(torch.float32, "pretrain_real")
+    assert abs(loss.item() - float(d["loss"])) < 1e-4, (loss.item(), float(d["loss"]))
+    np.testing.assert_allclose(answer.cpu().numpy(), d["answer_score"], rtol=1e-4, atol=1e-5)
+    pred = m.last_prediction_scores.float()
+    assert tuple(pred.shape[-1:]) == (30522,)
+    rows = [0, 1, 200, 392]
+    np.testing.assert_allclose(pred[:, rows].cpu().numpy(), d["i::prediction_rows"], rtol=1e-4,
+                               atol=1e-4)
+    lse = torch.logsumexp(pred.double(), -1).cpu().numpy()
+    np.testing.assert_allclose(lse, d["i::prediction_lse"], rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(m.last_seq_relationship.detach().cpu().numpy(),
+                               d["i::seq_relationship"], rtol=1e-4, atol=1e-5)
+    grads = {k: p.grad for k, p in m.named_parameters()}
+    _sample_check(d, grads, fp32=True)
+    gn = sum(float((g.double() ** 2).sum()) for g in grads.values()) ** 0.5
+    assert abs(gn - float(d["grad_norm"])) < 1e-3 * float(d["grad_norm"])
+
+
+@pytest.mark.gpu
+def test_pretrain_real_shape_bf16_close_to_reference():
+    """bf16 perf mode at the real config-2 shape: loss 2e-2, LM-head rows relative L2 <= 2e-2,
+    every row's logsumexp within 2e-2 nats, gradient samples' direction cosine > 0.98."""
+    meta, d, m, loss, losses, answer = _run(torch.bfloat16, "pretrain_real")
+    ref = float(d["loss"])
+    assert abs(loss.item() - ref) < 2e-2 * abs(ref), (loss.item(), ref)
+    pred = m.last_prediction_scores.float()
+    got = pred[:, [0, 1, 200, 392]].cpu().numpy().astype(np.float64)
+    want = d["i::prediction_rows"].astype(np.float64)
+    assert np.linalg.norm(got - want) <= 2e-2 * np.linalg.norm(want)
+    lse = torch.logsumexp(pred.double(), -1).cpu().numpy()
+    assert np.abs(lse - d["i::prediction_lse"]).max() < 2e-2
+    grads = {k: p.grad for k, p in m.named_parameters()}
+    _sample_check(d, grads, fp32=False)
