@@ -1,0 +1,105 @@
+"""Ordering parity that can fail: beam-search orders on stories whose best ordering wins by a
+DECISIVE margin (tests/golden/make_golden_real.py `make_decisive`: counter weights with the
+pointer's tanh_linear / pw_k / key_linear scaled, reference beam order + the reference's pointer
+NLL of every one of the 5! orders). Reference: modeling_bert.py:1405-1552, generator.py:15-38.
+
+fp32 parity mode: the beam order equals the reference's and the NLL of the best, second-best,
+worst and three more orders match the reference's (north_star 1e-4 on the loss = NLL / 4).
+bf16 perf mode (the benchmarked dtype): the bf16 error of the MARGIN (second-best minus best
+NLL, bf16 model vs the reference's) is measured per story; where the margin exceeds DECISIVE x
+that error the bf16 beam order must equal the reference's EXACTLY; the others are reported as
+near-ties. The fixtures were made so that the check cannot be vacuous (tools/decisive_probe.py):
+the config-3 story and at least half the tiny stories must be decisive, so a bf16 regression
+that moves the margins fails the test either way.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from counter_init import counter_state_dict
+from golden_util import GOLDEN
+from make_golden_real import real_inputs, scale_decisive
+
+pytestmark = pytest.mark.gpu
+FIXTURES = ["decisive_tiny", "decisive_config3"]
+
+if torch.cuda.is_available():
+    from multimodal_sequencing_amd import model_zoo
+    from multimodal_sequencing_amd.berson import berson_pointer_network
+
+
+def _load(name):
+    meta = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    return meta, dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+DECISIVE = 5.0  # margin / bf16 margin error above which the order must be exact
+
+
+def _model(name, meta, dtype):
+    m = model_zoo.build_from_golden(meta["config"], device="cuda", dtype=dtype)
+    sd = m.state_dict()
+    cw = scale_decisive(counter_state_dict({k: tuple(v.shape) for k, v in sd.items()}), name)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in cw.items()})
+    m.eval()
+    return m
+
+
+def _stories(meta):
+    ids, labels, images = real_inputs(meta["input_seed"], meta["config"])
+    for b in range(ids.shape[0]):
+        yield b, {"input_ids": torch.from_numpy(ids[b:b + 1]),
+                  "labels": torch.from_numpy(labels[b:b + 1]),
+                  "images": torch.from_numpy(images[b:b + 1]).cuda()}
+
+
+def _nll(m, inp, order):
+    """Pointer NLL of `order` = its beam score (the teacher-forced pointer loss x (N - 1))."""
+    with torch.no_grad():
+        m({**inp, "labels": torch.tensor([list(order)])})
+    return float(m.last_loss_terms[0]) * (len(order) - 1)
+
+
+def _picks(nll):
+    srt = np.argsort(nll)
+    rng = np.random.RandomState(0)
+    return [int(srt[0]), int(srt[1]), int(srt[-1])] + [int(x) for x in rng.choice(len(nll), 3, replace=False)]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_decisive_order_fp32(name):
+    meta, d = _load(name)
+    m = _model(name, meta, torch.float32)
+    for b, inp in _stories(meta):
+        ref = [int(x) for x in d["order"][b]]
+        assert berson_pointer_network(m.args, m, None, inp) == ref, (name, b)
+        for j in _picks(d["perm_nll"][b]):
+            got = _nll(m, inp, d["perms"][j])
+            want = float(d["perm_nll"][b, j])
+            assert abs(got - want) < 4e-4 * max(1.0, abs(want)), (name, b, d["perms"][j], got, want)
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_decisive_order_bf16_exact(name):
+    meta, d = _load(name)
+    m = _model(name, meta, torch.bfloat16)
+    decisive = 0
+    for b, inp in _stories(meta):
+        ref = [int(x) for x in d["order"][b]]
+        srt = np.argsort(d["perm_nll"][b])
+        best, second = int(srt[0]), int(srt[1])
+        assert list(d["perms"][best]) == ref  # the reference's beam found the optimum
+        margin = float(d["perm_nll"][b, second] - d["perm_nll"][b, best])
+        gap16 = _nll(m, inp, d["perms"][second]) - _nll(m, inp, d["perms"][best])
+        err = abs(gap16 - margin)
+        order = berson_pointer_network(m.args, m, None, inp)
+        print(f"{name} story {b}: margin {margin:.4f} nats, bf16 margin error {err:.2e} "
+              f"(x{margin / max(err, 1e-12):.1f}), bf16 order {order}, reference {ref}")
+        if margin > DECISIVE * err:
+            decisive += 1
+            assert order == ref, (name, b, order, ref, margin, err)
+    n = d["order"].shape[0]
+    assert decisive >= (n + 1) // 2, (name, decisive, n)  # the check is not vacuous
