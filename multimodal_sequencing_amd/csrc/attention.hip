@@ -552,6 +552,30 @@ __device__ __forceinline__ void settle(const V& v) { asm volatile("" ::"v"(v)); 
 __device__ __forceinline__ f32x4 mma(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// max / sum over lanes l, l ^ 16, l ^ 32, l ^ 48 with the gfx950 row swaps (no ds_bpermute, no
+// lane index arithmetic): permlane16_swap pairs rows (0,1), (2,3); permlane32_swap the two halves
+__device__ __forceinline__ float xlane_max4(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float m = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const uint32_t w = __float_as_uint(m);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
+__device__ __forceinline__ float xlane_sum4(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float m = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const uint32_t w = __float_as_uint(m);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+// A operand of all-ones (bf16 1.0): mma(ONES, P, acc) adds each query column's sum of P to all
+// four of its accumulator rows
+__device__ __forceinline__ bf16x8_t bf16_ones() {
+  const u16x8 v = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
 __device__ __forceinline__ rsrc_t head_rsrc(const void* base, int64_t row0, int64_t ld, int64_t col,
                                             int T) {
   const unsigned short* b = reinterpret_cast<const unsigned short*>(base) + row0 * ld + col;
@@ -642,6 +666,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
 
   f32x4 o[2][4];
   float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+  f32x4 lsum[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  const bf16x8_t ones = bf16_ones();
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp)
 #pragma unroll
@@ -709,8 +735,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
           }
         }
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xlane_max4(mx);
       // lazy rescaling: the running max only moves (and O, l are rescaled) when some row's tile
       // max exceeds it by more than 8 (log2 units), so unrescaled probabilities stay <= 2^8;
       // O / l and the LSE m + log2(l) are exact for any reference m
@@ -718,12 +743,13 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         const float mn = fmaxf(m[grp], mx);
         const float alpha = ex2(m[grp] - mn);
         m[grp] = mn;
-        l[grp] *= alpha;
+        if (DROP) l[grp] *= alpha;
+        else lsum[grp] *= alpha;
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[grp][d] *= alpha;
       }
       const float mn = m[grp];
-      float rs = 0.f;
+      float rs = 0.f;  // DROP only: without dropout the row sum is an MFMA of P (lsum)
       if (zb) {
         const float nm = -mn;
 #pragma unroll
@@ -732,7 +758,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
           for (int r = 0; r < 4; ++r) {
             const float e = ex2(fmaf(s[grp][kb][r], c, nm));
             s[grp][kb][r] = e;
-            rs += e;
+            if (DROP) rs += e;
           }
       } else {
 #pragma unroll
@@ -745,11 +771,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
           for (int r = 0; r < 4; ++r) {
             const float e = ex2(s[grp][kb][r] - mn);
             s[grp][kb][r] = e;
-            rs += e;
+            if (DROP) rs += e;
           }
         }
       }
-      l[grp] += rs;
+      if (DROP) l[grp] += rs;
       if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax);
                    // dropped scores are zeroed here, the 1/(1-p) of the kept ones is applied with
                    // the final normalisation (one integer compare feeds select and keep bit)
@@ -786,14 +812,19 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         if (nkb > 2) o[grp][d] = mma(v1, pf[grp][1], o[grp][d]);
       }
     }
+    if (!DROP) {  // row sums of the bf16 P that the PV product consumed: two MFMAs, no VALU adds
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        lsum[grp] = mma(ones, pf[grp][0], lsum[grp]);
+        if (nkb > 2) lsum[grp] = mma(ones, pf[grp][1], lsum[grp]);
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!active) return;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
-    float lt = l[grp];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = DROP ? xlane_sum4(l[grp]) : lsum[grp][0];
     const int q = qw + grp * 16 + i;
     if (q < T) {
       const float inv = (DROP ? a.drop.scale : 1.0f) / lt;

@@ -77,11 +77,7 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
   if (BWD) {
     if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
-      for (int r = 0; r < 8; r += 2) {
-        const f32x2 d = gelu_bwd_pair((f32x2){bf2f(in.x[r]), bf2f(in.x[r + 1])});
-        v[r] *= d[0];
-        v[r + 1] *= d[1];
-      }
+      for (int r = 0; r < 8; ++r) v[r] *= gelu_sig_grad(bf2f(in.x[r]));
     } else {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] *= act_bwd_fast(ACT, bf2f(in.x[r]));
@@ -90,11 +86,7 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
     if (a.aux) st8(reinterpret_cast<us*>(a.aux) + off, v);
     if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
-      for (int r = 0; r < 8; r += 2) {
-        const f32x2 y = gelu_fwd_pair((f32x2){v[r], v[r + 1]});
-        v[r] = y[0];
-        v[r + 1] = y[1];
-      }
+      for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
     } else {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
@@ -129,11 +121,7 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
   }
   if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
-    for (int r = 0; r < 8; r += 2) {
-      const f32x2 y = gelu_fwd_pair((f32x2){v[r], v[r + 1]});
-      v[r] = y[0];
-      v[r + 1] = y[1];
-    }
+    for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
   } else if (ACT) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);

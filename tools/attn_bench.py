@@ -39,7 +39,7 @@ def run(P, T, heads, drop, iters=5, bits=False, variant=1):
 
 
 variants = [int(v) for v in sys.argv[1:]] or [1, 2]
-for P, T in ((320, 513), (320, 393), (320, 512)):
+for P, T in ((640, 513), (640, 393)):
     for drop, bits in ((False, False), (True, True)):
         for var in variants:
             print(json.dumps({"P": P, "T": T, "drop": drop, "bits": bits, "variant": var,
