@@ -63,9 +63,28 @@ __device__ __forceinline__ EpiBias epi_bias(const GemmArgs& a, int n) {
   return b;
 }
 
-template <int ACT, bool BWD, bool XIN>
+// Activation-derivative table for the dgrad epilogues (dY * act'(z), z = the stored bf16
+// pre-activation): act'(z) for every bf16 z with 2^-10 <= |z| < 8 (13 binades x 128 mantissas x
+// 2 signs = 3328 fp32 entries, 13 KB of LDS), exact (libm erf / exp at kernel start). |z| outside
+// clamps to the range ends, where act' is within 8e-4 of its limit (0.5 near 0; 0 or 1 beyond 8).
+// One LDS gather per element instead of ~17 VALU slots of a fitted GELU' (two transcendentals).
+constexpr int DT_LO = 117 << 7;  // bf16 bits of 2^-10
+constexpr int DT_N = 13 * 128;   // entries per sign
+__device__ __forceinline__ int dtab_index(unsigned short u) {
+  const int a = min(max((int)(u & 0x7FFFu) - DT_LO, 0), DT_N - 1);
+  return a + (int)(u >> 15) * DT_N;
+}
+template <int ACT>
+__device__ __forceinline__ void dtab_fill(float MMSEQ_LDS* tab) {
+  for (int e = threadIdx.x; e < 2 * DT_N; e += blockDim.x) {
+    const unsigned short u = (unsigned short)(((e / DT_N) << 15) | (e % DT_N + DT_LO));
+    tab[e] = act_bwd(ACT, bf2f(u));
+  }
+}
+
+template <int ACT, bool BWD, bool XIN, bool DTAB = false>
 __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi, const EpiIn& in,
-                                     const EpiBias& bias) {
+                                     const EpiBias& bias, const float MMSEQ_LDS* dtab = nullptr) {
   if (m >= a.M || n >= a.N) return;
   float v[8];
 #pragma unroll
@@ -75,7 +94,10 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
   }
   const int64_t off = (int64_t)m * a.ldc + n;
   if (BWD) {
-    if (ACT == MMSEQ_ACT_GELU_ERF) {
+    if (DTAB) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] *= dtab[dtab_index(in.x[r])];
+    } else if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] *= gelu_sig_grad(bf2f(in.x[r]));
     } else {
@@ -205,11 +227,14 @@ __device__ __forceinline__ int g8_of(int X, int q) {
 template <int ACT, bool BWD, bool XIN, bool Q8 = false>  // Q8: MX-fp8 output (epi8_q8)
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles,
                                                             int delay) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF];  // 128 KB
+  // 128 KB of K-tile buffers, then (dgrad variants) the 13 KB activation-derivative table
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int G = gridDim.x;
+  float MMSEQ_LDS* dtab = (float MMSEQ_LDS*)(smem + 2 * 2 * G_LDA_HALF);
+  if (BWD) dtab_fill<ACT>(dtab);  // read after the prologue's barrier
   // XCD-aware order: the G/8 blocks sharing an XCD take consecutive tiles (shared A panels in L2)
   const int bid = blockIdx.x;
   const int first = xcd_item(bid, G);
@@ -395,7 +420,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     if (XIN) {
       // batches of 4 calls; the operand loads of batch h + 1 are issued before the stores of batch
       // h, and each batch is consumed (settled) once, so its wait never covers a store (vmcnt
-      // retires in issue order; a consume inside the per-call bounds branches would wait vmcnt(0))
+      // retires in issue order; a consume inside the per-call bounds branches would wait vmcnt(0)).
+      // (Three or four batches in flight spill: the fragment registers are not reused here.)
       EpiIn in[2][2][2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -418,9 +444,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int t = 0; t < 2; ++t)
-            epi8<ACT, BWD, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
-                                 t ? bias1 : bias0);
+            epi8<ACT, BWD, true, BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                      acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
+                                      t ? bias1 : bias0, dtab);
       }
     } else if (Q8) {
 #pragma unroll

@@ -22,7 +22,7 @@ def main():
     model.train()
     opt = FusedAdamW(model.stores(), lr=5e-6, warmup=100)
     data = bench.synthetic_batch(32, preset["N"], preset["per_seq"], 50265, 224, dev, seed=1000)
-    mbs = [{k: v[o:o + 16] for k, v in data.items()} for o in (0, 16)]
+    mbs = [data]  # bench.py's default: the whole 32-story batch in one micro-batch
     train_step(model, opt, mbs, None)
     torch.cuda.synchronize()
     recs = []
@@ -34,8 +34,11 @@ def main():
         e0.record(s)
         orig(A, B, C, M, Nn, K, **kw)
         e1.record(s)
-        key = (str(A.dtype).replace("torch.", ""), kw.get("trans", 0), M, Nn, K,
-               "acc" if kw.get("accumulate") else "")
+        epi = "".join(t for t, on in (("acc+", kw.get("accumulate")), ("res+", kw.get("resid") is not None),
+                                      ("drop+", kw.get("drop") is not None), (f"act{kw.get('act', 0)}+", kw.get("act")),
+                                      ("dact+", kw.get("dact") is not None), ("aux+", kw.get("aux") is not None),
+                                      ("bias+", kw.get("bias") is not None)) if on)
+        key = (str(A.dtype).replace("torch.", ""), kw.get("trans", 0), M, Nn, K, epi or "plain")
         recs.append((key, e0, e1))
 
     N.gemm = wrapped
@@ -51,7 +54,7 @@ def main():
     for key, (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
         dt, tr, M, Nn, K, acc = key
         tf = 2.0 * M * Nn * K * n / (ms * 1e-3) / 1e12
-        print(f"{dt:9s} tr={tr} M={M:7d} N={Nn:5d} K={K:7d} {acc:3s} calls={n:4d} {ms:8.2f} ms "
+        print(f"{dt:9s} tr={tr} M={M:7d} N={Nn:5d} K={K:7d} {acc:18s} calls={n:4d} {ms:8.2f} ms "
               f"{tf:7.1f} TF/s")
 
 

@@ -45,6 +45,8 @@ def main():
             r["plain"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K)) / 1e12
             r["gelu_aux"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, bias=bias, act=1, aux=aux)) / 1e12
             r["drop_res"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, bias=bias, resid=res, drop=d)) / 1e12
+            r["res"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, bias=bias, resid=res)) / 1e12
+            r["drop"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, bias=bias, drop=d)) / 1e12
             r["dgelu"] = fl / t(lambda: N.gemm(A, W, C, R, Nn, K, act=1, dact=res)) / 1e12
             print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}),
                   flush=True)
