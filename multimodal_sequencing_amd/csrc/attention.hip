@@ -43,6 +43,9 @@ struct AttnArgs {
   Drop drop;  // attention-probability dropout
   uint64_t* bits;  // bf16 fast path: keep-mask words [(p*heads+h)*T + q][nkt2], bit j = key 64*kt + j
   int nkt2;        // key tiles per row, rounded up to even (16-byte rows for the dK/dV staging)
+  // tail fold (bf16 dK/dV kernel): when 1 <= T % 128 <= 16 the last 128-row block of each (pair,
+  // head) also owns rows tail0 .. T-1 (tail0 = 128 * (T / 128)); 0 = no fold. nxq = row blocks.
+  int tail0, nxq;
 };
 
 // Stage rows [r0, r0+64) of one head's 64-wide slice into LDS tile s ([64][LD]); zero-fill >= T.
@@ -599,7 +602,33 @@ __device__ __forceinline__ BlkIdx attn_block(int nx, int heads) {
 }
 
 // ---- forward ---------------------------------------------------------------------------------
-template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep bits out
+// keep bits of a packed bf16 pair from one dropout hash word: half u of word x is kept iff
+// u >= thr (as drop_sel). Packed 16-bit ops, no compares: s = sat(u - (thr - 1)) is >= 1 exactly
+// when kept, k = min(s, 1) is the keep bit of each half and 0 - k its 16-bit AND mask (inline asm:
+// the compiler turns the elementwise form back into two compares and four selects)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t keep_bits2(uint32_t x, uint32_t thr1x2, uint32_t ones) {
+  uint32_t t, k;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(t) : "v"(x), "s"(thr1x2));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(k) : "v"(t), "v"(ones));
+  return k;
+}
+__device__ __forceinline__ uint32_t keep_mask2(uint32_t k) {
+  uint32_t m;
+  asm("v_pk_sub_u16 %0, 0, %1" : "=v"(m) : "v"(k));
+  return m;
+}
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {  // a value the compiler cannot
+  asm("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));                  // rematerialise inside the loop
+  return x;
+}
+__device__ __forceinline__ uint32_t hash_mixed(uint32_t x) {  // drop_mix with the final xor-shift
+  x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu;       // (whose halves drop_sel compares) last
+  return x ^ (x >> 16);
+}
+
+template <int DMODE, bool WIDE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep bits out;
+                                 // WIDE: dropout pair indices >= 2^32 (64-bit index arithmetic)
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
@@ -660,12 +689,16 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
   const float c = a.scale * LOG2E;
   const int Tp2 = (T + 1) & ~1;
   uint64_t drow[2];
+  uint32_t prow[2];  // narrow pair index of (row, key 4g) in tile 0
 #pragma unroll
-  for (int grp = 0; grp < 2; ++grp)
+  for (int grp = 0; grp < 2; ++grp) {
     drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp2;
+    prow[grp] = opaque_u32((uint32_t)(drow[grp] >> 1) + 2 * g);
+  }
+  const uint32_t thr1x2 = (a.drop.thr - 1) * 0x10001u, ones2 = opaque_u32(0x10001u);
 
   f32x4 o[2][4];
-  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+  float m[2] = {-1e30f, -1e30f};
   f32x4 lsum[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
   const bf16x8_t ones = bf16_ones();
 #pragma unroll
@@ -743,23 +776,17 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         const float mn = fmaxf(m[grp], mx);
         const float alpha = ex2(m[grp] - mn);
         m[grp] = mn;
-        if (DROP) l[grp] *= alpha;
-        else lsum[grp] *= alpha;
+        lsum[grp] *= alpha;
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[grp][d] *= alpha;
       }
       const float mn = m[grp];
-      float rs = 0.f;  // DROP only: without dropout the row sum is an MFMA of P (lsum)
       if (zb) {
         const float nm = -mn;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float e = ex2(fmaf(s[grp][kb][r], c, nm));
-            s[grp][kb][r] = e;
-            if (DROP) rs += e;
-          }
+          for (int r = 0; r < 4; ++r) s[grp][kb][r] = ex2(fmaf(s[grp][kb][r], c, nm));
       } else {
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
@@ -768,40 +795,48 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
             continue;
           }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float e = ex2(s[grp][kb][r] - mn);
-            s[grp][kb][r] = e;
-            if (DROP) rs += e;
-          }
+          for (int r = 0; r < 4; ++r) s[grp][kb][r] = ex2(s[grp][kb][r] - mn);
         }
-      }
-      if (DROP) l[grp] += rs;
-      if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax);
-                   // dropped scores are zeroed here, the 1/(1-p) of the kept ones is applied with
-                   // the final normalisation (one integer compare feeds select and keep bit)
-        uint32_t kb16 = 0;
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-          if (kb >= nkb) continue;  // all keys >= T: p = 0, keep bits never read
-          const uint64_t pr = (drow[grp] + t * 64 + kb * 16 + 4 * g) >> 1;
-#pragma unroll
-          for (int q2 = 0; q2 < 2; ++q2) {
-            const uint32_t h = drop_hash(a.drop, pr + q2);
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-              const int r = 2 * q2 + hf;
-              const bool keep = (hf ? (h >> 16) : (h & 0xFFFFu)) >= a.drop.thr;
-              s[grp][kb][r] = keep ? s[grp][kb][r] : 0.f;
-              if (DMODE == 2) kb16 |= (keep ? 1u : 0u) << (kb * 4 + r);
-            }
-          }
-        }
-        if (DMODE == 2)  // rows q >= T fall outside the descriptor and are dropped
-          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)kb16, rbits,
-                                                    boff0 + grp * 16 * a.nkt2 * 8 + t * 8, 0, 0);
       }
       pf[grp][0] = pack_pair(s[grp][0], s[grp][1]);
       pf[grp][1] = pack_pair(s[grp][2], s[grp][3]);
+      // row sums of the bf16 P (undropped: dropout acts after the softmax normalisation) by MFMA
+      lsum[grp] = mma(ones, pf[grp][0], lsum[grp]);
+      if (nkb > 2) lsum[grp] = mma(ones, pf[grp][1], lsum[grp]);
+      if (DROP) {  // dropped scores are zeroed in the packed P (one AND per pair of keys), the
+                   // 1/(1-p) of the kept ones is applied with the final normalisation.
+                   // dword j = 2 kb + q2 of the packed P holds keys 16 kb + 4g + 2 q2 + {0, 1}: the
+                   // two halves of one hash word, keep bits 2j and 2j + 1 of the row's 16-bit slice
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 w[2] = {__builtin_bit_cast(u32x4, pf[grp][0]), __builtin_bit_cast(u32x4, pf[grp][1])};
+        uint32_t acc = 0;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          if (kb >= nkb) continue;  // all keys >= T: p = 0, keep bits never read
+#pragma unroll
+          for (int q2 = 0; q2 < 2; ++q2) {
+            uint32_t hx;
+            if (WIDE) {
+              hx = drop_hash(a.drop, ((drow[grp] + t * 64 + kb * 16 + 4 * g) >> 1) + q2);
+            } else {  // drop_hash with the pair index < 2^32 (its high word 0)
+              const uint32_t x = ((prow[grp] + (uint32_t)(t * 32 + kb * 8 + q2)) ^ a.drop.k0) + a.drop.k1;
+              hx = hash_mixed(x ^ (x >> 16));
+            }
+            const uint32_t k = keep_bits2(hx, thr1x2, ones2);
+            const int j = 2 * kb + q2;
+            w[kb >> 1][j & 3] &= keep_mask2(k);
+            if (DMODE == 2) acc |= k << (2 * j);
+          }
+        }
+        pf[grp][0] = __builtin_bit_cast(bf16x8_t, w[0]);
+        pf[grp][1] = __builtin_bit_cast(bf16x8_t, w[1]);
+        if (DMODE == 2) {  // bits 2j (low halves) and 16 + 2j (high halves) -> 2j and 2j + 1
+          const uint32_t kb16 = (acc & 0x5555u) | ((acc >> 15) & 0xAAAAu);
+          // rows q >= T fall outside the descriptor and are dropped
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)kb16, rbits,
+                                                boff0 + grp * 16 * a.nkt2 * 8 + t * 8, 0, 0);
+        }
+      }
     }
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -812,19 +847,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
         if (nkb > 2) o[grp][d] = mma(v1, pf[grp][1], o[grp][d]);
       }
     }
-    if (!DROP) {  // row sums of the bf16 P that the PV product consumed: two MFMAs, no VALU adds
-#pragma unroll
-      for (int grp = 0; grp < 2; ++grp) {
-        lsum[grp] = mma(ones, pf[grp][0], lsum[grp]);
-        if (nkb > 2) lsum[grp] = mma(ones, pf[grp][1], lsum[grp]);
-      }
-    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!active) return;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
-    const float lt = DROP ? xlane_sum4(l[grp]) : lsum[grp][0];
+    const float lt = lsum[grp][0];
     const int q = qw + grp * 16 + i;
     if (q < T) {
       const float inv = (DROP ? a.drop.scale : 1.0f) / lt;
@@ -1317,13 +1345,22 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   float* sD = sL + nqt * 64;
   // keep-bit words of the q-tile for this block's two key tiles: [2 buffers][64 q][4 dwords]
   unsigned short* sBits = reinterpret_cast<unsigned short*>(sD + nqt * 64);
+  // tail fold (a.tail0 > 0, see tail_fold): the tail keys' keep words [2][64 q][4 dwords] and their
+  // K / V row fragments [4][64 lanes] x 16 B
+  unsigned short* sBitsT = sBits + 1024;
+  u16x8* sKVt = reinterpret_cast<u16x8*>(sBitsT + 1024);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
-  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const BlkIdx bi = attn_block(a.nxq, a.heads);
   const int h = bi.h, p = bi.p;
   const int kw = bi.x * 128 + wave * 32;
   const bool active = kw < T;
+  // tail block: it also owns keys tail0 .. T-1 (one 16-key group); the query sweep of that group is
+  // split over the waves (wave w takes the 16-query block w of every tile) and the four partial
+  // dK / dV tiles are summed in wave order at the end (deterministic); not in the counter-hash mode
+  // (DMODE 1: its registers go to the hashed keep masks; the host does not fold it)
+  const bool tailb = DMODE != 1 && a.tail0 > 0 && bi.x == a.nxq - 1;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
   const rsrc_t ro = head_rsrc(a.dout, (int64_t)p * T, a.ld_dout, h * 64, T);
@@ -1343,6 +1380,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     if (DMODE == 2 && wave == 0)  // 64 rows x 16 B: words (kt0, kt0 + 1) of queries t*64 + lane
       dma16(rbits, sBits + (t & 1) * 512,
             (uint32_t)((((int64_t)(t * 64 + lane)) * a.nkt2 + kt0) * 8));
+    if (DMODE == 2 && tailb && wave == 1)  // words (kt0 + 2, kt0 + 3): the tail keys' tile
+      dma16(rbits, sBitsT + (t & 1) * 512,
+            (uint32_t)((((int64_t)(t * 64 + lane)) * a.nkt2 + kt0 + 2) * 8));
   };
   stage(0);
   const int64_t rb = ((int64_t)p * a.heads + h) * T;
@@ -1373,17 +1413,32 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     }
     settle(kb2[grp]);
   }
+  float kb2t = -1e30f;
+  if (tailb) {
+    const int key = a.tail0 + i;
+    if (wave == 0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        sKVt[ks * 64 + lane] = __builtin_bit_cast(u16x8, glob_row_frag(Kb, ld, key, T, ks, lane));
+        sKVt[(2 + ks) * 64 + lane] = __builtin_bit_cast(u16x8, glob_row_frag(Vb, ld, key, T, ks, lane));
+      }
+    }
+    kb2t = key < T ? (kbias ? kbias[key] * LOG2E : 0.f) : -1e30f;
+    settle(kb2t);
+  }
   const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
   int to[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
   const int Tp2 = (T + 1) & ~1;
-  f32x4 dk[2][4], dv[2][4];
+  f32x4 dk[2][4], dv[2][4], dkt[4], dvt[4];
 #pragma unroll
-  for (int grp = 0; grp < 2; ++grp)
+  for (int d = 0; d < 4; ++d) {
+    dkt[d] = dvt[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int d = 0; d < 4; ++d) dk[grp][d] = dv[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int grp = 0; grp < 2; ++grp) dk[grp][d] = dv[grp][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
   for (int t = 0; t < nqt; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1483,8 +1538,81 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
         }
       }
     }
+    if (tailb) {  // the tail keys against this wave's 16-query block of the tile
+      asm volatile("" ::: "memory");  // keeps this work in the branch (not speculated into every block)
+      const int qs = wave, ks = wave >> 1;
+      const bf16x8_t q0 = lds_row(qimg, qs * 1024 + ro0), q1 = lds_row(qimg, qs * 1024 + ro1);
+      const bf16x8_t o0 = lds_row(oimg, qs * 1024 + ro0), o1 = lds_row(oimg, qs * 1024 + ro1);
+      f32x4 st = mma(q0, __builtin_bit_cast(bf16x8_t, sKVt[lane]), (f32x4){0.f, 0.f, 0.f, 0.f});
+      st = mma(q1, __builtin_bit_cast(bf16x8_t, sKVt[64 + lane]), st);
+      f32x4 dpt = mma(o0, __builtin_bit_cast(bf16x8_t, sKVt[128 + lane]), (f32x4){0.f, 0.f, 0.f, 0.f});
+      dpt = mma(o1, __builtin_bit_cast(bf16x8_t, sKVt[192 + lane]), dpt);
+      const f32x4 Lq = *reinterpret_cast<const f32x4*>(sL + t * 64 + qs * 16 + 4 * g);
+      const f32x4 Dq = *reinterpret_cast<const f32x4*>(sD + t * 64 + qs * 16 + 4 * g);
+      // DMODE 2: tail key j = i of its tile: bit ((i >> 2) & 3) * 16 + (i & 3), dword (i >> 3) & 1
+      const uint32_t* bwt = reinterpret_cast<const uint32_t*>(sBitsT + (t & 1) * 512) + ((i >> 3) & 1);
+      const uint32_t post = ((i >> 2) & 1) * 16 + (i & 3);
+      const uint64_t dbt = (uint64_t)(rb + t * 64 + qs * 16 + 4 * g) * (uint64_t)Tp2 + a.tail0 + i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = ex2(fmaf(st[r], c, kb2t) - Lq[r]);
+        float mk = 1.f;
+        if (DMODE == 2)
+          mk = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)bwt[(qs * 16 + 4 * g + r) * 4], post, 1) & scale_u);
+        if (DMODE == 1) mk = drop_mul(a.drop, dbt + (uint64_t)r * Tp2);
+        st[r] = pv * mk;
+        dpt[r] = pv * fmaf(dpt[r], mk, -Dq[r]);
+      }
+      // the block's 16 queries sit in the low (qs even) or high (qs odd) half of k-step ks
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const bf16x8_t pft = (qs & 1) ? pack_pair(z, st) : pack_pair(st, z);
+      const bf16x8_t dsft = (qs & 1) ? pack_pair(z, dpt) : pack_pair(dpt, z);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8_t ov = lds_tr(oimg, ks * 32 * 64 + to[d]);
+        const bf16x8_t qv = lds_tr(qimg, ks * 32 * 64 + to[d]);
+        dvt[d] = mma(ov, pft, dvt[d]);
+        dkt[d] = mma(qv, dsft, dkt[d]);
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (tailb) {  // every wave of the tail block is active (its first key is < T)
+    float* red = reinterpret_cast<float*>(smem);  // [3 waves][32 floats][64 lanes] = 24 KB
+    __syncthreads();  // all waves are past their last LDS read of the images
+    if (wave > 0) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          red[((wave - 1) * 32 + d * 4 + r) * 64 + lane] = dkt[d][r];
+          red[((wave - 1) * 32 + 16 + d * 4 + r) * 64 + lane] = dvt[d][r];
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dkt[d][r] += red[(w * 32 + d * 4 + r) * 64 + lane];
+            dvt[d][r] += red[(w * 32 + 16 + d * 4 + r) * 64 + lane];
+          }
+      const int key = a.tail0 + i;
+      if (key < T) {
+        unsigned short* row = reinterpret_cast<unsigned short*>(a.dqkv) + ((int64_t)p * T + key) * a.ld_dqkv;
+        unsigned short* dkp = row + a.k_off + h * 64 + 4 * g;
+        unsigned short* dvp = row + a.v_off + h * 64 + 4 * g;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          Vec4<unsigned short>::st(dkp + d * 16, dkt[d] * a.scale);
+          Vec4<unsigned short>::st(dvp + d * 16, dvt[d]);
+        }
+      }
+    }
+  }
   if (!active) return;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
@@ -1503,6 +1631,21 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// Row blocks of the tail-folding kernels: T = 128 n + r with 1 <= r <= 16 (T = 513, 393, 769 on the
+// path) runs n blocks, the last one also owning the r tail rows, instead of n + 1 blocks whose last
+// has one active wave; a block's time is set by its key sweep, not by how many of its rows are valid
+// (DESIGN §7), so the n + 1-th block cost a full block. MMSEQ_ATTN_NO_FOLD=1 at build time: off.
+void tail_fold(AttnArgs& a, int T) {  // T = 0: no fold (a.nxq from a.T)
+  const int n = T / 128, r = T % 128;
+#ifndef MMSEQ_ATTN_NO_FOLD
+  const bool fold = n >= 1 && r >= 1 && r <= 16;
+#else
+  const bool fold = false;
+#endif
+  a.tail0 = fold ? n * 128 : 0;
+  a.nxq = fold ? n : (a.T + 127) / 128;
+}
 
 mmseq_status check_common(int P, int T, int heads, const void* qkv, int64_t ld, int64_t qo,
                           int64_t ko, int64_t vo, mmseq_dtype dt) {
@@ -1558,12 +1701,16 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;
     a.bits = keep_bits;
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
+    // largest dropout pair index + the in-tile key offset must stay below 2^32 for the narrow path
+    const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 1) & ~1)) / 2 + 64 >= (1ull << 32);
     if (a.drop.thr && keep_bits)
-      hipLaunchKernelGGL(attn_fwd_bf16_kernel<2>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL((wide ? attn_fwd_bf16_kernel<2, true> : attn_fwd_bf16_kernel<2, false>), gq,
+                         dim3(256), lds, s, a);
     else if (a.drop.thr)
-      hipLaunchKernelGGL(attn_fwd_bf16_kernel<1>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL((wide ? attn_fwd_bf16_kernel<1, true> : attn_fwd_bf16_kernel<1, false>), gq,
+                         dim3(256), lds, s, a);
     else
-      hipLaunchKernelGGL(attn_fwd_bf16_kernel<0>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL((attn_fwd_bf16_kernel<0, false>), gq, dim3(256), lds, s, a);
   } else if (dtype == MMSEQ_BF16)
     hipLaunchKernelGGL(attn_fwd_kernel<unsigned short>, grid, dim3(256), 0, s, a);
   else
@@ -1603,15 +1750,25 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2 + 2048;
     a.bits = const_cast<uint64_t*>(keep_bits);
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
-    if (a.drop.thr && keep_bits) {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<2>, gq, dim3(256), lds, s, a);
-    } else if (a.drop.thr) {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<1>, gq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<1>, gq, dim3(256), lds, s, a);
+    // dK/dV tail fold: + the tail keys' keep words (2 KB) and K / V fragments (4 KB); the counter-
+    // hash mode (no keep bits) runs unfolded (its registers are spent on the hashed keep masks)
+    const int dmode = a.drop.thr ? (keep_bits ? 2 : 1) : 0;
+    AttnArgs ak = a;
+    tail_fold(ak, dmode == 1 ? 0 : T);
+    const size_t ldsk = lds + (ak.tail0 ? 6144 : 0);
+    // the dQ kernel does not fold: its tail state took it from three to two waves per SIMD
+    // (148 -> 236 VGPRs), slower at T = 513 and 393 than the extra block it saves
+    tail_fold(a, 0);
+    const dim3 gdq((unsigned)(a.nxq * heads * P)), gdk((unsigned)(ak.nxq * heads * P));
+    if (dmode == 2) {
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gdq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<2>, gdk, dim3(256), ldsk, s, ak);
+    } else if (dmode == 1) {
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<1>, gdq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<1>, gdk, dim3(256), ldsk, s, ak);
     } else {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<0>, gq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<0>, gq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<0>, gdq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<0>, gdk, dim3(256), ldsk, s, ak);
     }
   } else if (dtype == MMSEQ_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<unsigned short>, gd, dim3(256), 0, s, a);

@@ -21,6 +21,8 @@ CANDIDATES = {
     "tl200": {"tanh_linear.weight": 200},
     "tl50_q50": {"tanh_linear.weight": 50, "query_linear.weight": 50},
     "tl100_pw10": {"tanh_linear.weight": 100, "pw_k.weight": 10},
+    "tl50_q50_kl50": {"tanh_linear.weight": 50, "query_linear.weight": 50, "key_linear.weight": 50},
+    "tl20_q200": {"tanh_linear.weight": 20, "query_linear.weight": 200},
 }
 
 
@@ -41,10 +43,16 @@ def nll(m, inp, order):
 
 
 def main():
-    for cname, cfg, seed in (("tiny", DECISIVE_TINY, 311), ("config3", CONFIG3, 310)):
+    # usage: decisive_probe.py [config3_stories [candidate ...]] (default: both fixtures, B as made)
+    B3 = int(sys.argv[1]) if len(sys.argv) > 1 else CONFIG3["B"]
+    names = sys.argv[2:] or list(CANDIDATES)
+    runs = (("config3", dict(CONFIG3, B=B3), 310),) if len(sys.argv) > 1 else \
+        (("tiny", DECISIVE_TINY, 311), ("config3", CONFIG3, 310))
+    for cname, cfg, seed in runs:
         ids, labels, images = real_inputs(seed, cfg)
         perms = list(itertools.permutations(range(cfg["N"])))
-        for sname, scale in CANDIDATES.items():
+        for sname in names:
+            scale = CANDIDATES[sname]
             m32, m16 = model(cfg, torch.float32, scale), model(cfg, torch.bfloat16, scale)
             rows = []
             for b in range(ids.shape[0]):
