@@ -629,7 +629,10 @@ __device__ __forceinline__ uint32_t hash_mixed(uint32_t x) {  // drop_mix with t
 
 template <int DMODE, bool WIDE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep bits out;
                                  // WIDE: dropout pair indices >= 2^32 (64-bit index arithmetic)
-__global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(AttnArgs a) {
+#ifndef MMSEQ_ATTN_FWD_WPE
+#define MMSEQ_ATTN_FWD_WPE 3  // forward workgroups per CU the register budget is sized for
+#endif
+__global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
   float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
@@ -1698,7 +1701,10 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   } else if (dtype == MMSEQ_BF16 && variant) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
-    const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;
+    size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;
+#ifdef MMSEQ_ATTN_FWD_LDS_PAD  // occupancy experiments: pad the workgroup's LDS
+    lds += MMSEQ_ATTN_FWD_LDS_PAD;
+#endif
     a.bits = keep_bits;
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
     // largest dropout pair index + the in-tile key offset must stay below 2^32 for the narrow path
