@@ -123,6 +123,14 @@ mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld
                             float scale, void* out, int64_t ld_out, float* lse,
                             mmseq_dtype dtype, const mmseq_dropout* drop, uint64_t* keep_bits,
                             int variant, mmseq_stream stream);
+/* attn_fwd_mxfp8: the bf16 fast forward without dropout (eval) whose output O [P*T][heads*64] is
+ *  written in MX-fp8 (mmseq_quant_mxfp8 layout, bit-identical to quantising the bf16 output; the
+ *  scales of the rows past P*T up to the next multiple of 64 are left to the caller) for the output
+ *  projection's fp8 GEMM (BASELINE config 5; lxrt/modeling.py:398-425, clip/model.py:219-221). */
+mmseq_status mmseq_attn_fwd_mxfp8(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                  int64_t q_off, int64_t k_off, int64_t v_off,
+                                  const float* key_bias, float scale, float* lse, void* q8,
+                                  int64_t ldq8, void* q8_scales, mmseq_stream stream);
 mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, const void* out, int64_t ld_out, const void* dout,
@@ -170,6 +178,15 @@ mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, mmseq_rows x
                                  mmseq_rows yl, float* mean, float* rstd, mmseq_dtype x_dtype,
                                  mmseq_dtype y_dtype, const mmseq_dropout* drop_y,
                                  mmseq_stream stream);
+/* layernorm_fwd_mxfp8: bf16 LayerNorm (no dropout) that also writes its output in the MX-fp8 format
+ *  of mmseq_quant_mxfp8 (q [rows][ldq] e4m3 + packed scales, bit-identical to quantising the bf16
+ *  output), the A operand of the next fp8 GEMM (BASELINE config 5: QKV and FC1 after the LNs of
+ *  lxrt/modeling.py:431-439,485-493 and clip/model.py:221-225). cols in {256, 512, 768, 1024};
+ *  y may be null when the GEMM is its only consumer. */
+mmseq_status mmseq_layernorm_fwd_mxfp8(int rows, int cols, const void* x, mmseq_rows xl,
+                                       const float* gamma, const float* beta, float eps, void* y,
+                                       mmseq_rows yl, float* mean, float* rstd, void* q,
+                                       int64_t ldq, void* q_scales, mmseq_stream stream);
 int64_t mmseq_layernorm_bwd_workspace(int rows, int cols);
 mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
                                  const void* x, mmseq_rows xl, const float* mean,
@@ -387,6 +404,14 @@ mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int64_t lda,
 mmseq_status mmseq_gemm_mxfp8_out(int M, int N, int K, const void* A, int64_t lda, const void* B,
                                   int64_t ldb, const float* bias, int act, void* q, int64_t ldq,
                                   void* scales, mmseq_stream stream);
+/* gemm_mxfp8_q8: MX-fp8 GEMM (A, B and scales as mmseq_gemm_mxfp8) whose output is MX-fp8 as in
+ *  mmseq_gemm_mxfp8_out: q [M][N] e4m3 + q_scales = quant(bf16(act(A B^T + bias))), for the MLP's
+ *  FC1 -> FC2 chain with both GEMMs on the fp8 MFMA (lxrt/modeling.py:467-493, clip/model.py:
+ *  208-214). K % 256 == 0, N % 32 == 0, 16-byte aligned operands, lda / ldb / ldq % 16 == 0. */
+mmseq_status mmseq_gemm_mxfp8_q8(int M, int N, int K, const void* A, int64_t lda,
+                                 const void* a_scales, const void* B, int64_t ldb,
+                                 const void* b_scales, const float* bias, int act, void* q,
+                                 int64_t ldq, void* q_scales, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * CLIP ModifiedResNet / RN50 (clip/model.py:10-187; lxrt/modeling.py:621-705, 1014-1030), NHWC.

@@ -68,6 +68,9 @@ _SIGS = {
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            ctypes.c_int, _dp, _vp, ctypes.c_int,
                                                            _vp]),
+    "mmseq_attn_fwd_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
+                                                           _vp, ctypes.c_float, _vp, _vp, _c_i64,
+                                                           _vp, _vp]),
     "mmseq_attn_keep_bits_words": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
@@ -81,6 +84,9 @@ _SIGS = {
     "mmseq_layernorm_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, _vp,
                                            ctypes.c_float, _vp, Rows, _vp, _vp, ctypes.c_int,
                                            ctypes.c_int, _dp, _vp]),
+    "mmseq_layernorm_fwd_mxfp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, _vp,
+                                                 ctypes.c_float, _vp, Rows, _vp, _vp, _vp, _c_i64,
+                                                 _vp, _vp]),
     "mmseq_layernorm_bwd_workspace": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
     "mmseq_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
                                            _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
@@ -130,6 +136,9 @@ _SIGS = {
     "mmseq_gemm_mxfp8_out": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _c_i64, _vp,
                                                                 ctypes.c_int, _vp, _c_i64, _vp,
                                                                 _vp]),
+    "mmseq_gemm_mxfp8_q8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
+                                                               _vp, ctypes.c_int, _vp, _c_i64, _vp,
+                                                               _vp]),
     "mmseq_conv_im2col": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_conv_col2im": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_bn_workspace": (ctypes.c_int64, [_c_i64, ctypes.c_int]),
@@ -305,6 +314,19 @@ def layernorm_fwd(nrows, cols, x, xl, gamma, beta, eps, y, yl, mean, rstd, drop=
     _check(lib().mmseq_layernorm_fwd(nrows, cols, _p(x), xl, _p(gamma), _p(beta), eps, _p(y), yl,
                                      _p(mean), _p(rstd), dt(x), dt(y), _d(drop), _stream()),
            "mmseq_layernorm_fwd")
+
+
+def layernorm_fwd_mxfp8(nrows, cols, x, gamma, beta, eps, y=None, mean=None, rstd=None):
+    """LayerNorm of x [nrows][cols] bf16 (unit row stride layout) -> MXFP8 of the output (+ the bf16
+    output into y when given) in one pass (mmseq_layernorm_fwd_mxfp8)."""
+    _dev(x, gamma, beta)
+    ldq = (cols + 15) // 16 * 16
+    q = torch.empty(nrows, ldq, dtype=torch.uint8, device=x.device)
+    sc = torch.empty(lib().mmseq_mxfp8_scale_bytes(nrows, cols), dtype=torch.uint8, device=x.device)
+    _check(lib().mmseq_layernorm_fwd_mxfp8(nrows, cols, _p(x), rows(cols), _p(gamma), _p(beta), eps,
+                                           _p(y), rows(cols), _p(mean), _p(rstd), _p(q), ldq,
+                                           _p(sc), _stream()), "mmseq_layernorm_fwd_mxfp8")
+    return MXFP8(q, sc, nrows, cols)
 
 
 def layernorm_bwd(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl, dgamma,
@@ -516,6 +538,18 @@ def quant_mxfp8(x, out=None):
     return out
 
 
+def attn_fwd_mxfp8(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, lse):
+    """Eval attention forward whose output is MX-fp8 (mmseq_attn_fwd_mxfp8): MXFP8 [P*T][heads*64],
+    the output projection's fp8 operand; padding-row scales zeroed here."""
+    rows_, cols = P * T, heads * 64
+    q = torch.empty(rows_, (cols + 15) // 16 * 16, dtype=torch.uint8, device=qkv.device)
+    sc = torch.zeros(lib().mmseq_mxfp8_scale_bytes(rows_, cols), dtype=torch.uint8, device=qkv.device)
+    _check(lib().mmseq_attn_fwd_mxfp8(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off,
+                                      _p(key_bias), scale, _p(lse), _p(q), q.stride(0), _p(sc),
+                                      _stream()), "mmseq_attn_fwd_mxfp8")
+    return MXFP8(q, sc, rows_, cols)
+
+
 def gemm_mxfp8(a, b, c, bias=None, act=0, resid=None, alpha=1.0):
     """c[m][n] (bf16) = act(alpha * a @ b^T + bias) + resid, a / b MXFP8 operands."""
     if a.K != b.K or tuple(c.shape) != (a.rows, b.rows) or c.dtype != torch.bfloat16:
@@ -541,6 +575,20 @@ def gemm_mxfp8_out(x, W, bias=None, act=0):
     _check(lib().mmseq_gemm_mxfp8_out(rows, Nn, K, _p(x), x.stride(0), _p(W), W.stride(0),
                                       _p(bias), act, _p(q), q.stride(0), _p(sc), _stream()),
            "mmseq_gemm_mxfp8_out")
+    return MXFP8(q, sc, rows, Nn)
+
+
+def gemm_mxfp8_q8(a, b, bias=None, act=0):
+    """MXFP8 of bf16(act(a @ b^T + bias)) for MXFP8 operands a [rows][K], b [N][K]
+    (mmseq_gemm_mxfp8_q8): an fp8 GEMM whose output is the next fp8 GEMM's A operand."""
+    if a.K != b.K:
+        raise ValueError("gemm_mxfp8_q8: K mismatch")
+    rows, Nn = a.rows, b.rows
+    q = torch.empty(rows, (Nn + 15) // 16 * 16, dtype=torch.uint8, device=a.q.device)
+    sc = torch.empty(lib().mmseq_mxfp8_scale_bytes(rows, Nn), dtype=torch.uint8, device=a.q.device)
+    _check(lib().mmseq_gemm_mxfp8_q8(rows, Nn, a.K, _p(a.q), a.q.stride(0), _p(a.scales), _p(b.q),
+                                     b.q.stride(0), _p(b.scales), _p(bias), act, _p(q), q.stride(0),
+                                     _p(sc), _stream()), "mmseq_gemm_mxfp8_q8")
     return MXFP8(q, sc, rows, Nn)
 
 

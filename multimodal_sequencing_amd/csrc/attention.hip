@@ -46,6 +46,9 @@ struct AttnArgs {
   // tail fold (bf16 dK/dV kernel): when 1 <= T % 128 <= 16 the last 128-row block of each (pair,
   // head) also owns rows tail0 .. T-1 (tail0 = 128 * (T / 128)); 0 = no fold. nxq = row blocks.
   int tail0, nxq;
+  // bf16 forward, Q8: the output in MX-fp8 (fp8.hip layout) instead of bf16: e4m3 [P*T][ldq8] +
+  // packed scales for (P*T, heads*64) columns
+  uint8_t* q8; int64_t ldq8; uint8_t* q8s;
 };
 
 // Stage rows [r0, r0+64) of one head's 64-wide slice into LDS tile s ([64][LD]); zero-fill >= T.
@@ -627,8 +630,9 @@ __device__ __forceinline__ uint32_t hash_mixed(uint32_t x) {  // drop_mix with t
   return x ^ (x >> 16);
 }
 
-template <int DMODE, bool WIDE>  // dropout: 0 none, 1 counter hash, 2 counter hash + keep bits out;
-                                 // WIDE: dropout pair indices >= 2^32 (64-bit index arithmetic)
+template <int DMODE, bool WIDE, bool Q8 = false>  // dropout: 0 none, 1 counter hash, 2 counter
+                                 // hash + keep bits out; WIDE: dropout pair indices >= 2^32 (64-bit
+                                 // index arithmetic); Q8: MX-fp8 output (eval, the O-proj operand)
 #ifndef MMSEQ_ATTN_FWD_WPE
 #define MMSEQ_ATTN_FWD_WPE 3  // forward workgroups per CU the register budget is sized for
 #endif
@@ -859,10 +863,41 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
     const int q = qw + grp * 16 + i;
     if (q < T) {
       const float inv = (DROP ? a.drop.scale : 1.0f) / lt;
-      unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
-                           h * 64 + 4 * g;
+      if (Q8) {  // MX-fp8 of the bf16-rounded output (bit-identical to bf16 out + mmseq_quant_mxfp8):
+                 // block b of the head's 64 columns = d 2b, 2b+1 of the four lanes g of query i
+        const int64_t row = (int64_t)p * T + q;
+        const int KB = a.heads * 2;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(op + d * 16, o[grp][d] * inv);
+        for (int b = 0; b < 2; ++b) {
+          float v[8], amax = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] = bf2f(f2bf(o[grp][2 * b + (e >> 2)][e & 3] * inv));
+            amax = fmaxf(amax, fabsf(v[e]));
+          }
+          amax = xlane_max4(amax);
+          int ex = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
+          ex = max(-127, min(127, ex - 8));
+          const float sc = ldexpf(1.f, -ex);
+          if (g == 0)
+            a.q8s[((row >> 6) * KB + h * 2 + b) * 64 + (row & 15) * 4 + ((row >> 4) & 3)] = (uint8_t)(ex + 127);
+#pragma unroll
+          for (int dd = 0; dd < 2; ++dd) {
+            const float s0 = fminf(448.f, fmaxf(-448.f, v[4 * dd] * sc));
+            const float s1 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 1] * sc));
+            const float s2 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 2] * sc));
+            const float s3 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 3] * sc));
+            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+            *reinterpret_cast<int*>(a.q8 + row * a.ldq8 + h * 64 + (2 * b + dd) * 16 + 4 * g) = pk;
+          }
+        }
+      } else {
+        unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
+                             h * 64 + 4 * g;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(op + d * 16, o[grp][d] * inv);
+      }
       if (g == 0) a.lse[((int64_t)p * a.heads + h) * T + q] = (m[grp] + __builtin_amdgcn_logf(lt)) * LN2;
     }
   }
@@ -1791,4 +1826,29 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
 extern "C" int64_t mmseq_attn_keep_bits_words(int P, int T, int heads) {
   const int64_t nkt2 = (((T + 63) / 64) + 1) & ~1;
   return (int64_t)P * heads * T * nkt2;
+}
+
+extern "C" mmseq_status mmseq_attn_fwd_mxfp8(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                             int64_t q_off, int64_t k_off, int64_t v_off,
+                                             const float* key_bias, float scale, float* lse,
+                                             void* q8, int64_t ldq8, void* q8_scales,
+                                             mmseq_stream stream) {
+  mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, MMSEQ_BF16);
+  if (st) return st;
+  MMSEQ_REQUIRE(lse && q8 && q8_scales && ldq8 >= heads * 64 && ldq8 % 16 == 0 &&
+                    ((uintptr_t)q8 & 15) == 0,
+                "attn_fwd_mxfp8: bad output (ldq8 % 16, 16-byte aligned)");
+  if (P == 0) return MMSEQ_OK;
+  AttnArgs a = {};
+  a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
+  a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
+  a.lse = lse; a.drop = make_drop(nullptr);
+  a.q8 = reinterpret_cast<uint8_t*>(q8); a.ldq8 = ldq8; a.q8s = reinterpret_cast<uint8_t*>(q8_scales);
+  const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
+  const int nkt = (T + 63) / 64;
+  const size_t lds = (size_t)4 * 4096 * 2 + (size_t)nkt * (64 + 1) * 4;
+  a.nkt2 = (nkt + 1) & ~1;
+  hipLaunchKernelGGL((attn_fwd_bf16_kernel<0, false, true>), gq, dim3(256), lds,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return mmseq_check_launch("attn_fwd_mxfp8");
 }

@@ -347,6 +347,23 @@ extern "C" mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int
   MMSEQ_REQUIRE(((uintptr_t)C & 7) == 0 && (!resid || ((uintptr_t)resid & 7) == 0),
                 "gemm_mxfp8: 8-byte aligned output");
   if (M == 0) return MMSEQ_OK;
+#ifndef MMSEQ_F8_OLD
+  {  // the 256 x 256 8-phase schedule (gemm256.hip, F8) when K % 256 == 0 and there are tiles for it
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+    g.bias = bias; g.act = act; g.resid = resid; g.ldr = ldr; g.alpha = alpha;
+    g.splitk = 1; g.kchunk = K; g.drop = make_drop(nullptr);
+    g.f8_sa = (const uint8_t*)a_scales; g.f8_sb = (const uint8_t*)b_scales;
+    g.f8_sa_bytes = mmseq_mxfp8_scale_bytes(M, K); g.f8_sb_bytes = mmseq_mxfp8_scale_bytes(N, K);
+    hipError_t e = hipSuccess;
+    if (M >= 256 && N >= 256 &&
+        mmseq_gemm256_nt_f8(g, mmseq_device_cus(), reinterpret_cast<hipStream_t>(stream), &e)) {
+      if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_mxfp8 launch: %s", hipGetErrorString(e));
+      return mmseq_check_launch("gemm_mxfp8");
+    }
+  }
+#endif
   // 256 x 256 tiles once there are rows and columns for them, else 128 x 128
   const bool wide = M >= 512 && N >= 256;
   const int tile = wide ? 256 : 128;
@@ -390,4 +407,34 @@ extern "C" mmseq_status mmseq_gemm_mxfp8_out(int M, int N, int K, const void* A,
                 "gemm_mxfp8_out: preconditions");
   if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_mxfp8_out launch: %s", hipGetErrorString(e));
   return mmseq_check_launch("gemm_mxfp8_out");
+}
+
+extern "C" mmseq_status mmseq_gemm_mxfp8_q8(int M, int N, int K, const void* A, int64_t lda,
+                                            const void* a_scales, const void* B, int64_t ldb,
+                                            const void* b_scales, const float* bias, int act,
+                                            void* q, int64_t ldq, void* q_scales,
+                                            mmseq_stream stream) {
+  MMSEQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 256 == 0 && N % 32 == 0,
+                "gemm_mxfp8_q8: K % 256 and N % 32 must be 0");
+  MMSEQ_REQUIRE(lda >= K && ldb >= K && lda % 16 == 0 && ldb % 16 == 0 && ldq >= N && ldq % 16 == 0,
+                "gemm_mxfp8_q8: leading dimensions");
+  MMSEQ_REQUIRE(A && B && a_scales && b_scales && q && q_scales, "gemm_mxfp8_q8: null buffer");
+  MMSEQ_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && ((uintptr_t)q & 15) == 0,
+                "gemm_mxfp8_q8: 16-byte alignment");
+  MMSEQ_REQUIRE(act == 0 || act == MMSEQ_ACT_GELU_ERF || act == MMSEQ_ACT_QUICKGELU,
+                "gemm_mxfp8_q8: act");
+  if (M == 0) return MMSEQ_OK;
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K;
+  g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = q; g.ldc = ldq;
+  g.bias = bias; g.act = act; g.alpha = 1.f; g.splitk = 1; g.kchunk = K;
+  g.drop = make_drop(nullptr);
+  g.q8_scales = reinterpret_cast<uint8_t*>(q_scales);
+  g.f8_sa = (const uint8_t*)a_scales; g.f8_sb = (const uint8_t*)b_scales;
+  g.f8_sa_bytes = mmseq_mxfp8_scale_bytes(M, K); g.f8_sb_bytes = mmseq_mxfp8_scale_bytes(N, K);
+  hipError_t e = hipSuccess;
+  MMSEQ_REQUIRE(mmseq_gemm256_nt_f8(g, mmseq_device_cus(), reinterpret_cast<hipStream_t>(stream), &e),
+                "gemm_mxfp8_q8: preconditions");
+  if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_mxfp8_q8 launch: %s", hipGetErrorString(e));
+  return mmseq_check_launch("gemm_mxfp8_q8");
 }

@@ -248,11 +248,37 @@ __device__ __forceinline__ int g8_of(int X, int q) {
   return 4 + (q & 3) + ((q >> 2) << 3);
 }
 
-template <int ACT, bool BWD, bool XIN, bool Q8 = false>  // Q8: MX-fp8 output (epi8_q8)
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+// the fp8 MFMA operand of a lane = its two 16-byte chunks ks = 0, 1 of the 128-byte row (K positions
+// 16g .. 16g + 15 and 64 + 16g .. 64 + 16g + 15, the layout fp8.hip probed): exactly the two bf16
+// fragments the same lane reads for the two 32-deep k-steps of a bf16 K-tile
+__device__ __forceinline__ i32x8 cat8(const bf16x8_t& lo, const bf16x8_t& hi) {
+  const i32x4 l = __builtin_bit_cast(i32x4, lo), h = __builtin_bit_cast(i32x4, hi);
+  return (i32x8){l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+}
+
+// the block-scaled fp8 MFMA with its accumulator tied (dst = srcC) by an inline-asm constraint: the
+// builtin form lets the register allocator move every accumulator to a fresh tuple, which in the
+// 256-register 8-wave kernel spills 140-165 VGPRs
+__device__ __forceinline__ void mfma_f8_acc(f32x4& c, const i32x8& a, const i32x8& b, uint32_t sa,
+                                            uint32_t sb) {
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+               : "+v"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+}
+
+// Q8: MX-fp8 output (epi8_q8). F8: MX-fp8 operands (BASELINE config 5's fp8 MFMA path): the same
+// schedule with 128-byte K-tiles of 128 e4m3 (one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16
+// output tile and phase, twice the FLOPs of the bf16 phase in the same cycles), plus the K-tile's
+// E8M0 scales (256 B per 64-row group, one 16-lane LDS-DMA per wave, staged with half-tile A_hi)
+template <int ACT, bool BWD, bool XIN, bool Q8 = false, bool F8 = false>
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tiles_n, int ntiles,
                                                             int delay) {
-  // 128 KB of K-tile buffers, then (dgrad variants) the 13 KB activation-derivative table
-  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0)];
+  // 128 KB of K-tile buffers, then (dgrad variants) the 13 KB activation-derivative table or (F8)
+  // the 2 x 2 KB scale buffers
+  __shared__ __attribute__((aligned(16))) unsigned short
+      smem[2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0) + (F8 ? 2048 : 0)];
+  unsigned short* const sscale = smem + 2 * 2 * G_LDA_HALF;  // F8: [2 buffers][A 1 KB | B 1 KB]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -269,37 +295,51 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)delay) __builtin_amdgcn_s_sleep(8);
   }
-  const int nk = a.K >> 6;
-  const unsigned short* Ab = reinterpret_cast<const unsigned short*>(a.A);
-  const unsigned short* Bb = reinterpret_cast<const unsigned short*>(a.B);
+  const int nk = F8 ? a.K >> 7 : a.K >> 6;  // 128-byte K-tiles
+  const int64_t lda_b = F8 ? a.lda : 2 * a.lda, ldb_b = F8 ? a.ldb : 2 * a.ldb;  // row bytes
+  const int64_t kbytes = F8 ? a.K : 2 * a.K;
+  const uint8_t* Ab = reinterpret_cast<const uint8_t*>(a.A);
+  const uint8_t* Bb = reinterpret_cast<const uint8_t*>(a.B);
+  const int KB32 = a.K >> 5;  // F8: E8M0 blocks per row
 
   // per-lane source offsets (bytes) for a 1 KB piece = 8 rows x 128 B; the swizzle term
   // ((row >> 1) & 7) = (lane >> 4) | 4 * (g8 & 1) depends on the parity of the 8-row group
   const int lr = lane >> 3, lc = lane & 7;
-  const uint32_t offA0 = (uint32_t)(lr * a.lda * 2 + ((lc ^ (lane >> 4)) << 4));
-  const uint32_t offA1 = (uint32_t)(lr * a.lda * 2 + ((lc ^ ((lane >> 4) | 4)) << 4));
+  const uint32_t offA0 = (uint32_t)(lr * lda_b + ((lc ^ (lane >> 4)) << 4));
+  const uint32_t offA1 = (uint32_t)(lr * lda_b + ((lc ^ ((lane >> 4) | 4)) << 4));
   // B: swizzle term ((lane >> 4) & 1) | ((g8 & 3) << 1)
-  const uint32_t offB0 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ ((lane >> 4) & 1)) << 4));
-  const uint32_t offB1 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ (((lane >> 4) & 1) | 2)) << 4));
-  const uint32_t offB2 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ (((lane >> 4) & 1) | 4)) << 4));
-  const uint32_t offB3 = (uint32_t)(lr * a.ldb * 2 + ((lc ^ (((lane >> 4) & 1) | 6)) << 4));
+  const uint32_t offB0 = (uint32_t)(lr * ldb_b + ((lc ^ ((lane >> 4) & 1)) << 4));
+  const uint32_t offB1 = (uint32_t)(lr * ldb_b + ((lc ^ (((lane >> 4) & 1) | 2)) << 4));
+  const uint32_t offB2 = (uint32_t)(lr * ldb_b + ((lc ^ (((lane >> 4) & 1) | 4)) << 4));
+  const uint32_t offB3 = (uint32_t)(lr * ldb_b + ((lc ^ (((lane >> 4) & 1) | 6)) << 4));
 
   // operand descriptors of the current and the next tile, computed once per tile (the tile order
   // costs integer divisions): past the last tile a zero-size range (zero-fill, no traffic)
-  auto descs = [&](int tile, rsrc_t& ra, rsrc_t& rb) {
+  // F8: the scale arrays (one descriptor each for the whole kernel) and the first 64-row scale
+  // group of a tile's A / B rows; past the last tile, groups whose offsets fall outside the array
+  // (zero-fill, no traffic)
+  const rsrc_t rSA = make_rsrc(a.f8_sa, F8 ? a.f8_sa_bytes : 0);
+  const rsrc_t rSB = make_rsrc(a.f8_sb, F8 ? a.f8_sb_bytes : 0);
+  struct Sc { int ga, gb; };
+  auto descs = [&](int tile, rsrc_t& ra, rsrc_t& rb, Sc& sc) {
     if (tile < ntiles) {
       int tm, tn;
       tile_mn(tile, tiles_n, ntiles, tm, tn);
       const int m0 = tm * 256, n0 = tn * 256;
-      ra = make_rsrc(Ab + (int64_t)m0 * a.lda, ((int64_t)(a.M - m0 - 1) * a.lda + a.K) * 2);
-      rb = make_rsrc(Bb + (int64_t)n0 * a.ldb, ((int64_t)(a.N - n0 - 1) * a.ldb + a.K) * 2);
+      ra = make_rsrc(Ab + (int64_t)m0 * lda_b, (int64_t)(a.M - m0 - 1) * lda_b + kbytes);
+      rb = make_rsrc(Bb + (int64_t)n0 * ldb_b, (int64_t)(a.N - n0 - 1) * ldb_b + kbytes);
+      sc.ga = m0 >> 6;
+      sc.gb = n0 >> 6;
     } else {
       ra = rb = make_rsrc(Ab, 0);
+      sc.ga = (int)(a.f8_sa_bytes / 64 / (KB32 > 0 ? KB32 : 1));
+      sc.gb = (int)(a.f8_sb_bytes / 64 / (KB32 > 0 ? KB32 : 1));
     }
   };
   rsrc_t rAc, rBc, rAn, rBn;
-  descs(first, rAc, rBc);
-  descs(first + G, rAn, rBn);
+  Sc scc{}, scn{};
+  descs(first, rAc, rBc, scc);
+  descs(first + G, rAn, rBn, scn);
 
   // stage half-tile X of K-tile kk of the current tile (kk >= nk: the next tile's K-tile kk - nk)
   auto stage = [&](int it, int kk, int X) {
@@ -308,7 +348,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     if (nxt) kk -= nk;
     const bool isA = (X == 0 || X == 3);
     const rsrc_t r = isA ? (nxt ? rAn : rAc) : (nxt ? rBn : rBc);
-    const int64_t ld = isA ? a.lda : a.ldb;
+    const int64_t ld = isA ? lda_b : ldb_b;
     unsigned short* img = smem + (kk & 1) * (2 * G_LDA_HALF) + (isA ? 0 : G_LDA_HALF);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -317,8 +357,19 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
       const int gb = g8 & 3;
       const uint32_t lo = isA ? ((g8 & 1) ? offA1 : offA0)
                               : (gb == 0 ? offB0 : gb == 1 ? offB1 : gb == 2 ? offB2 : offB3);
-      const uint32_t voff = lo + (uint32_t)((g8 * 8 * ld + kk * 64) * 2);
+      const uint32_t voff = lo + (uint32_t)(g8 * 8 * ld + kk * 128);
       dma16(r, img + g8 * 512, voff);
+    }
+    if (F8 && X == 3) {  // the K-tile's scales: waves 0-3 the A groups, 4-7 the B groups (16 lanes)
+      const bool sa = wave < 4;
+      const int grp = (sa ? (nxt ? scn.ga : scc.ga) : (nxt ? scn.gb : scc.gb)) + (wave & 3);
+      const uint32_t so = (uint32_t)(((int64_t)grp * KB32 + 4 * kk) * 64 + lane * 16);
+      unsigned short* dst = sscale + (kk & 1) * 1024 + wave * 128;
+      if (sa) {
+        if (lane < 16) dma16(rSA, dst, so);
+      } else {
+        if (lane < 16) dma16(rSB, dst, so);
+      }
     }
   };
 
@@ -336,6 +387,40 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
 #define FRB(base, j, ks) __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>( \
       smem + (base) + (4 * ((j) & 1) + 32 * ((j) >> 1)) * 64 + ((ks) ? swb1 : swb0)))
 
+  // F8 scale dwords of the K-tile being computed (lane group b = lane >> 4 = its K block): A rows of
+  // fragment i are 16-row block i & 3 of 64-row group wr * 2 + (i >> 2) (byte i & 3 of dword
+  // i >> 2); B fragment j's permuted rows (brow / FRB) are all in group wc, row r64 = 8 (l15 >> 2) +
+  // (l15 & 3) + 4 (j & 1) + 32 (j >> 1): dword j & 1, byte (l15 >> 3) + 2 (j >> 1)
+  uint32_t scA[2] = {0u, 0u}, scB[2] = {0u, 0u};
+  const int scb_sh = 8 * (l15 >> 3);
+  const uint8_t* scbase = reinterpret_cast<const uint8_t*>(sscale) + (lane >> 4) * 64;
+  auto read_scales = [&](int h) {
+    const uint8_t* sp = scbase + h * 2048;
+    scA[0] = *reinterpret_cast<const uint32_t*>(sp + (wr * 2) * 256 + l15 * 4);
+    scA[1] = *reinterpret_cast<const uint32_t*>(sp + (wr * 2 + 1) * 256 + l15 * 4);
+    const int rb = 8 * ((l15 >> 2) & 1) + (l15 & 3);
+    scB[0] = *reinterpret_cast<const uint32_t*>(sp + 1024 + wc * 256 + rb * 4);
+    scB[1] = *reinterpret_cast<const uint32_t*>(sp + 1024 + wc * 256 + (rb + 4) * 4);
+  };
+#define QUAD(I0, I1, J0, J1)                                                                      \
+  if (F8) {                                                                                       \
+    uint32_t sa_[I1 - I0], sb_[J1 - J0];                                                          \
+    _Pragma("unroll") for (int i = I0; i < I1; ++i) sa_[i - I0] = scA[i >> 2] >> (8 * (i & 3));   \
+    _Pragma("unroll") for (int j = J0; j < J1; ++j)                                               \
+      sb_[j - J0] = scB[j & 1] >> (scb_sh + 16 * (j >> 1));                                       \
+    /* asm MFMAs are invisible to the hazard recognizer: the scale VGPRs written by VALU get */    \
+    /* explicit wait states before the first MFMA reads them */                                   \
+    asm volatile("s_nop 4" ::"v"(sa_[0]), "v"(sa_[I1 - I0 - 1]), "v"(sb_[0]), "v"(sb_[J1 - J0 - 1])); \
+    _Pragma("unroll") for (int i = I0; i < I1; ++i)                                               \
+    _Pragma("unroll") for (int j = J0; j < J1; ++j)                                               \
+      mfma_f8_acc(acc[i][j], fb8[j], fa8[i], sb_[j - J0], sa_[i - I0]);                           \
+  } else {                                                                                        \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                              \
+    _Pragma("unroll") for (int i = I0; i < I1; ++i)                                               \
+    _Pragma("unroll") for (int j = J0; j < J1; ++j)                                               \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0); \
+  }
+
   int it = 0;
   if (first >= ntiles) return;
   stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2); stage(0, 0, 3);
@@ -345,7 +430,18 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
 
   f32x4 acc[8][4];
-  bf16x8_t fa[8][2], fb[4][2];
+  bf16x8_t fa[8][2], fb[4][2];  // bf16: the fragments of the two 32-deep k-steps
+  i32x8 fa8[8], fb8[4];         // F8: the same bytes as one 8-register operand (no copies)
+#define LDA(i)                                                                  \
+  do {                                                                          \
+    if (F8) fa8[i] = cat8(FR(buf + arow, i, 0), FR(buf + arow, i, 1));          \
+    else { fa[i][0] = FR(buf + arow, i, 0); fa[i][1] = FR(buf + arow, i, 1); }  \
+  } while (0)
+#define LDB(j)                                                                  \
+  do {                                                                          \
+    if (F8) fb8[j] = cat8(FRB(buf + brow, j, 0), FRB(buf + brow, j, 1));        \
+    else { fb[j][0] = FRB(buf + brow, j, 0); fb[j][1] = FRB(buf + brow, j, 1); } \
+  } while (0)
   for (int tile = first; tile < ntiles; tile += G, ++it) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -358,60 +454,43 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
         const int buf = h * (2 * G_LDA_HALF);
         // ---- phase 1 (5): A_lo + B_lo, quadrant (i 0-3, j 0-1)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { fa[i][0] = FR(buf + arow, i, 0); fa[i][1] = FR(buf + arow, i, 1); }
+        for (int i = 0; i < 4; ++i) LDA(i);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) { fb[j][0] = FRB(buf + brow, j, 0); fb[j][1] = FRB(buf + brow, j, 1); }
+        for (int j = 0; j < 2; ++j) LDB(j);
+        if (F8) read_scales(h);
         if (h == 0) stage(it, 2 * s + 1, 2); else stage(it, 2 * s + 2, 2);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        QUAD(0, 4, 0, 2)
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         // ---- phase 2 (6): B_hi, quadrant (i 0-3, j 2-3)
 #pragma unroll
-        for (int j = 2; j < 4; ++j) { fb[j][0] = FRB(buf + brow, j, 0); fb[j][1] = FRB(buf + brow, j, 1); }
+        for (int j = 2; j < 4; ++j) LDB(j);
         if (h == 0) stage(it, 2 * s + 1, 3); else stage(it, 2 * s + 2, 3);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 2; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        QUAD(0, 4, 2, 4)
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         // ---- phase 3 (7): A_hi, quadrant (i 4-7, j 2-3)
 #pragma unroll
-        for (int i = 4; i < 8; ++i) { fa[i][0] = FR(buf + arow, i, 0); fa[i][1] = FR(buf + arow, i, 1); }
+        for (int i = 4; i < 8; ++i) LDA(i);
         if (h == 0) stage(it, 2 * s + 2, 0); else stage(it, 2 * s + 3, 0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 4; i < 8; ++i)
-#pragma unroll
-            for (int j = 2; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        QUAD(4, 8, 2, 4)
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -422,13 +501,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 4; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+        QUAD(4, 8, 0, 2)
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -436,6 +509,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     }
 
     // ---- epilogue (the next tile's first K-tiles are already in flight)
+    if (F8) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // asm MFMA results
     int tm, tn;
     tile_mn(tile, tiles_n, ntiles, tm, tn);
     const int m0 = tm * 256, n0 = tn * 256;
@@ -447,7 +521,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
       rAc = rAn;
       rBc = rBn;
-      descs(tile + 2 * G, rAn, rBn);
+      scc = scn;
+      descs(tile + 2 * G, rAn, rBn, scn);
       continue;
     }
     const EpiBias bias0 = epi_bias(a, n0 + wc * 64 + 8 * g), bias1 = epi_bias(a, n0 + wc * 64 + 32 + 8 * g);
@@ -500,10 +575,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     }
     rAc = rAn;
     rBc = rBn;
-    descs(tile + 2 * G, rAn, rBn);
+    scc = scn;
+    descs(tile + 2 * G, rAn, rBn, scn);
   }
 #undef FR
 #undef FRB
+#undef QUAD
+#undef LDA
+#undef LDB
   if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
@@ -938,6 +1017,41 @@ bool mmseq_gemm256_nt_q8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_
     hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, false, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
   else
     hipLaunchKernelGGL((gemm256_nt_kernel<0, false, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
+  *err = hipGetLastError();
+  return true;
+}
+
+// MX-fp8 operands (F8) on the 256 x 256 schedule: A e4m3 [M][lda], B e4m3 [N][ldb] + packed scales
+// (fp8.hip); bf16 out (bias, GELU / QuickGELU, residual) or, with a.q8_scales, MX-fp8 out.
+bool mmseq_gemm256_nt_f8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_t* err) {
+  auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  const bool q8 = a.q8_scales != nullptr;
+  if (a.K % 256 != 0 || a.splitk != 1 || a.lda % 16 != 0 || a.ldb % 16 != 0 || !a16(a.A) ||
+      !a16(a.B) || !a.f8_sa || !a.f8_sb || a.aux || a.dact || a.accumulate || a.drop.thr || !a16(a.C))
+    return false;
+  if (q8 ? (a.N % 32 != 0 || a.ldc % 16 != 0 || a.resid)
+         : (a.N % 8 != 0 || a.ldc % 8 != 0 || (a.resid && (a.ldr % 8 != 0 || !a16(a.resid)))))
+    return false;
+  if (a.act != 0 && a.act != MMSEQ_ACT_GELU_ERF && a.act != MMSEQ_ACT_QUICKGELU) return false;
+  const int tn = (a.N + 255) / 256;
+  const int ntiles = ((a.M + 255) / 256) * tn;
+  const dim3 grid(ntiles < num_cu ? ntiles : num_cu), block(512);
+#define F8_LAUNCH(ACT, XIN, Q8) \
+  hipLaunchKernelGGL((gemm256_nt_kernel<ACT, false, XIN, Q8, true>), grid, block, 0, s, a, tn, ntiles, 0)
+  if (q8) {
+    if (a.act == MMSEQ_ACT_GELU_ERF) F8_LAUNCH(MMSEQ_ACT_GELU_ERF, false, true);
+    else if (a.act == MMSEQ_ACT_QUICKGELU) F8_LAUNCH(MMSEQ_ACT_QUICKGELU, false, true);
+    else F8_LAUNCH(0, false, true);
+  } else if (a.resid) {
+    if (a.act == MMSEQ_ACT_GELU_ERF) F8_LAUNCH(MMSEQ_ACT_GELU_ERF, true, false);
+    else if (a.act == MMSEQ_ACT_QUICKGELU) F8_LAUNCH(MMSEQ_ACT_QUICKGELU, true, false);
+    else F8_LAUNCH(0, true, false);
+  } else {
+    if (a.act == MMSEQ_ACT_GELU_ERF) F8_LAUNCH(MMSEQ_ACT_GELU_ERF, false, false);
+    else if (a.act == MMSEQ_ACT_QUICKGELU) F8_LAUNCH(MMSEQ_ACT_QUICKGELU, false, false);
+    else F8_LAUNCH(0, false, false);
+  }
+#undef F8_LAUNCH
   *err = hipGetLastError();
   return true;
 }

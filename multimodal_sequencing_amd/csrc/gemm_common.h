@@ -17,6 +17,8 @@ struct GemmArgs {
   float* cs;       // TN wgrad: fused bias gradient cs[m] += sum_k A[k][m] (nullptr: off)
   float* cs_slab;  // ... per-split partials [splitk][M] when splitk > 1
   uint8_t* q8_scales;  // 256 NT kernel, MX-fp8 output: C is e4m3 [M][ldc] + these packed scales
+  // 256 NT kernel, MX-fp8 operands (F8): A / B are e4m3 [rows][ld] with these packed E8M0 scales
+  const uint8_t* f8_sa; const uint8_t* f8_sb; int64_t f8_sa_bytes, f8_sb_bytes;
 };
 
 template <typename TO>
@@ -122,6 +124,8 @@ bool mmseq_gemm256_nt(const mmseq_gemm_detail::GemmArgs& a, bool out_bf16, int n
 // ... with the activations written as MX-fp8 (e4m3 + packed E8M0 per 32 columns, fp8.hip
 // layout) instead of bf16: the consumer GEMM's A operand without a quantisation pass
 bool mmseq_gemm256_nt_q8(const mmseq_gemm_detail::GemmArgs& a, int num_cu, hipStream_t s,
+                         hipError_t* err);
+bool mmseq_gemm256_nt_f8(const mmseq_gemm_detail::GemmArgs& a, int num_cu, hipStream_t s,
                          hipError_t* err);
 // CU count of the current device (write-once per-device table, gemm.hip)
 int mmseq_device_cus();

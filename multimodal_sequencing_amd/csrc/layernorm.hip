@@ -268,6 +268,104 @@ __global__ __launch_bounds__(256) void ln_fwd16_kernel(int rows, int cols, const
   }
 }
 
+// LayerNorm forward (no dropout) whose output is also written as MX-fp8 for the next GEMM's A
+// operand (fp8.hip layout: e4m3 [rows][ldq], E8M0 per 32 columns, packed scales), bit-identical to
+// mmseq_quant_mxfp8 of the bf16 output: the bf16-rounded values are quantised. A 32-column block
+// is 4 consecutive lanes' 8 columns, so its amax takes two lane swaps. y may be null (the GEMM is
+// the only consumer). Blocks past the last row write the zero scales of the rows up to the next
+// multiple of 64 (as the quantiser does).
+template <int NJ>
+__global__ __launch_bounds__(256) void ln_fwd16_q8_kernel(int rows, int cols,
+                                                          const us* __restrict__ x, mmseq_rows xl,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          us* __restrict__ y, mmseq_rows yl,
+                                                          float* __restrict__ mean,
+                                                          float* __restrict__ rstd,
+                                                          uint8_t* __restrict__ q, int64_t ldq,
+                                                          uint8_t* __restrict__ qs) {
+  const int l = threadIdx.x & 31;
+  const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int KB = cols >> 5;
+  auto sidx = [&](int64_t row, int c) {
+    return ((row >> 6) * KB + (c >> 5)) * 64 + (row & 15) * 4 + ((row >> 4) & 3);
+  };
+  if (r >= rows) {  // zero scales of the padding rows up to the next multiple of 64
+    if (r < ((rows + 63) & ~63) && (l & 3) == 0) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) qs[sidx(r, (j * 32 + l) * 8)] = 0;
+    }
+    return;
+  }
+  const us* xr = x + row_off(xl, r);
+  u16x8 raw[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) raw[j] = *reinterpret_cast<const u16x8*>(xr + (j * 32 + l) * 8);
+  float v[NJ][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    unpack8(raw[j], v[j]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[j][e];
+  }
+  const float mu = hsum(s) / cols;
+  float qv = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[j][e] - mu;
+      qv = fmaf(d, d, qv);
+    }
+  const float rs = rsqrtf(hsum(qv) / cols + eps);
+  us* yr = y ? y + row_off(yl, r) : nullptr;
+  uint8_t* qr = q + r * ldq;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (j * 32 + l) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c), g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c), b1 = *reinterpret_cast<const f32x4*>(beta + c + 4);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = fmaf((v[j][e] - mu) * rs, g0[e], b0[e]);
+      o[4 + e] = fmaf((v[j][4 + e] - mu) * rs, g1[e], b1[e]);
+    }
+    const u16x8 ob = pack8(o);
+    if (yr) *reinterpret_cast<u16x8*>(yr + c) = ob;
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = bf2f(ob[e]);
+      amax = fmaxf(amax, fabsf(o[e]));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+    int ex = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
+    ex = max(-127, min(127, ex - 8));
+    const float inv = ldexpf(1.f, -ex);
+    if ((l & 3) == 0) qs[sidx(r, c)] = (uint8_t)(ex + 127);
+    uint32_t w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float s0 = fminf(448.f, fmaxf(-448.f, o[4 * h] * inv));
+      const float s1 = fminf(448.f, fmaxf(-448.f, o[4 * h + 1] * inv));
+      const float s2 = fminf(448.f, fmaxf(-448.f, o[4 * h + 2] * inv));
+      const float s3 = fminf(448.f, fmaxf(-448.f, o[4 * h + 3] * inv));
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+      w[h] = (uint32_t)pk;
+    }
+    typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+    *reinterpret_cast<u32x2*>(qr + c) = (u32x2){w[0], w[1]};
+  }
+  if (l == 0) {
+    if (mean) mean[r] = mu;
+    if (rstd) rstd[r] = rs;
+  }
+}
+
 // dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres); RPB16 rows per block,
 // each half wave walks rows hw, hw + 8, ... with the next row's loads issued before the current
 // row's math; per-block dgamma / dbeta partials -> ws[block][2][cols]
@@ -522,4 +620,30 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
   if (st) return st;
   if (dgamma || dbeta) return ln_reduce_partials(nb, cols, workspace, dgamma, dbeta, s);
   return MMSEQ_OK;
+}
+
+extern "C" mmseq_status mmseq_layernorm_fwd_mxfp8(int rows, int cols, const void* x, mmseq_rows xl,
+                                                  const float* gamma, const float* beta, float eps,
+                                                  void* y, mmseq_rows yl, float* mean, float* rstd,
+                                                  void* q, int64_t ldq, void* q_scales,
+                                                  mmseq_stream stream) {
+  MMSEQ_REQUIRE(rows >= 0 && cols % 256 == 0 && cols >= 256 && cols <= 1024,
+                "layernorm_fwd_mxfp8: cols must be 256, 512, 768 or 1024");
+  MMSEQ_REQUIRE(x && gamma && beta && q && q_scales && ldq >= cols && ldq % 16 == 0,
+                "layernorm_fwd_mxfp8: null buffer / ldq");
+  MMSEQ_REQUIRE(xl.rpb > 0 && (!y || yl.rpb > 0), "layernorm_fwd_mxfp8: rpb must be > 0");
+  MMSEQ_REQUIRE(rows_vec16(x, xl) && (!y || rows_vec16(y, yl)) && ((uintptr_t)gamma % 16) == 0 &&
+                    ((uintptr_t)beta % 16) == 0 && ((uintptr_t)q % 16) == 0,
+                "layernorm_fwd_mxfp8: 16-byte aligned rows");
+  if (rows == 0) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 g8((((rows + 63) & ~63) + 7) / 8);
+  switch (cols / 256) {
+#define LNQ(NJ) hipLaunchKernelGGL((ln_fwd16_q8_kernel<NJ>), g8, dim3(256), 0, s, rows, cols,       \
+                  (const us*)x, xl, gamma, beta, eps, (us*)y, yl, mean, rstd, (uint8_t*)q, ldq, \
+                  (uint8_t*)q_scales); break
+    case 1: LNQ(1); case 2: LNQ(2); case 3: LNQ(3); case 4: LNQ(4);
+#undef LNQ
+  }
+  return mmseq_check_launch("layernorm_fwd_mxfp8");
 }

@@ -46,11 +46,11 @@ def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=No
 
 # ------------------------------------------------------------------------------------------------
 # MX-fp8 inference GEMMs (BASELINE config 5): under `fp8_forward()`, the no-grad forward of the
-# encoder layers runs each MLP as FC1 + activation with an MX-fp8 epilogue (mmseq_gemm_mxfp8_out:
-# the activations leave the GEMM already quantised) and FC2 on the fp8 MFMA (mmseq_gemm_mxfp8, its
-# weight quantised once per store version). QKV and the attention output projection stay bf16: at
-# K = H their fp8 GEMM is no faster than bf16 and a separate activation quantisation pass would be
-# pure cost (profiles/r2s2_fp8_gemm_fastact.json). Training keeps bf16.
+# encoder layers runs QKV, the attention output projection, FC1 and FC2 on the fp8 MFMA (the 256 x
+# 256 8-phase schedule with MX-fp8 operands, gemm256.hip F8; weights quantised once per store
+# version, activations by mmseq_quant_mxfp8, FC1's output by its own epilogue for FC2). Shapes the
+# 8-phase form does not take (K or widths not multiples of 256) keep the round-2 path: FC1 bf16
+# with an MX-fp8 epilogue, FC2 fp8, QKV / O bf16. Training keeps bf16.
 _FP8 = {"on": False, "cache": {}}
 
 
@@ -80,14 +80,58 @@ def _fp8_weight(st, W):
     return hit[2]
 
 
-def _mlp_fwd(st, x, Wi, bi, act, Wo, bo, resid, lin):
-    """resid + FC2(act(FC1(x))) of a no-grad forward; under fp8_forward() (bf16, K % 128 == 0,
-    FC1 width % 128 == 0) FC1 writes MX-fp8 from its epilogue and FC2 runs on the fp8 MFMA."""
-    K, F = x.shape[-1], Wi.shape[0]
+def _f8(x, W):
+    """The no-grad forward runs this GEMM on the fp8 MFMA: fp8_forward() on, bf16, K and the output
+    width multiples of 256 (the 256 x 256 8-phase kernel's MX-fp8 form)."""
+    K = x.shape[-1]
+    return (_FP8["on"] and x.dtype == torch.bfloat16 and K % 256 == 0 and W.shape[0] % 256 == 0
+            and x.is_contiguous())
+
+
+def _mx(x):
+    """The MX-fp8 copy of activation x: the one its producer (a fused LayerNorm) attached, else a
+    quantisation pass (mmseq_quant_mxfp8)."""
+    q = getattr(x, "_mx", None)
+    return q if q is not None else N.quant_mxfp8(x.view(-1, x.shape[-1]))
+
+
+def _lin8(st, x, W, bias=None, resid=None, xq=None):
+    """bf16 act-free x W^T + bias (+ resid) with both operands in MX-fp8 (the activation's copy
+    from _mx or xq, the weight quantised once per store version)."""
+    xq = xq if xq is not None else _mx(x)
+    out = torch.empty(xq.rows, W.shape[0], device=W.device, dtype=torch.bfloat16)
+    N.gemm_mxfp8(xq, _fp8_weight(st, W), out, bias=bias,
+                 resid=resid.view(xq.rows, -1) if resid is not None else None)
+    return out
+
+
+def _ln8(x, gamma, beta, eps, y=None, mean=None, rstd=None):
+    """LayerNorm of x whose output also leaves in MX-fp8 (mmseq_layernorm_fwd_mxfp8); with y the
+    bf16 output too, its MX-fp8 copy attached for the next fp8 GEMM (_mx)."""
+    q = N.layernorm_fwd_mxfp8(x.shape[0], x.shape[-1], x, gamma, beta, eps, y=y, mean=mean, rstd=rstd)
+    if y is not None:
+        y._mx = q
+    return q
+
+
+def _mlp_fwd(st, x, Wi, bi, act, Wo, bo, resid, lin, xq=None):
+    """resid + FC2(act(FC1(x))) of a no-grad forward. Under fp8_forward(): with K and both widths
+    multiples of 256 both GEMMs run on the fp8 MFMA (FC1's epilogue writes FC2's MX-fp8 operand,
+    mmseq_gemm_mxfp8_q8); otherwise (K % 128 == 0) FC1 is the bf16 GEMM with that epilogue
+    (mmseq_gemm_mxfp8_out) and FC2 the fp8 GEMM."""
+    K, F = Wi.shape[1], Wi.shape[0]
+    if xq is not None:  # the input arrives in MX-fp8 only (fused LayerNorm)
+        q = N.gemm_mxfp8_q8(xq, _fp8_weight(st, Wi), bias=bi, act=act)
+        out = torch.empty(xq.rows, Wo.shape[0], device=Wi.device, dtype=torch.bfloat16)
+        N.gemm_mxfp8(q, _fp8_weight(st, Wo), out, bias=bo, resid=resid.view(xq.rows, -1))
+        return out
     if (_FP8["on"] and x.dtype == torch.bfloat16 and K % 128 == 0 and F % 128 == 0
             and x.is_contiguous() and resid.is_contiguous()):
         R = x.numel() // K
-        q = N.gemm_mxfp8_out(x.view(R, K), Wi, bias=bi, act=act)
+        if _f8(x, Wi) and F % 256 == 0 and Wo.shape[0] % 256 == 0:
+            q = N.gemm_mxfp8_q8(_mx(x), _fp8_weight(st, Wi), bias=bi, act=act)
+        else:
+            q = N.gemm_mxfp8_out(x.view(R, K), Wi, bias=bi, act=act)
         out = torch.empty(R, Wo.shape[0], device=x.device, dtype=x.dtype)
         N.gemm_mxfp8(q, _fp8_weight(st, Wo), out, bias=bo, resid=resid.view(R, -1))
         return out
@@ -163,9 +207,15 @@ class BertLayerFn(torch.autograd.Function):
         d_att, d_o, d_out = drops
         Wqkv = st.packed(L.qkv_w, "w")
         bqkv = st.packed(L.qkv_b, "f32").view(-1)
-        qkv = _linear(x, Wqkv, bias=bqkv)
-        o = torch.empty_like(x)
+        f8 = not save and _f8(x, Wqkv) and d_att is None and d_o is None
+        qkv = _lin8(st, x, Wqkv, bias=bqkv) if f8 else _linear(x, Wqkv, bias=bqkv)
         lse = torch.empty(P, heads, T, device=x.device)
+        if f8:  # eval: attention writes the output projection's MX-fp8 operand directly
+            oq = N.attn_fwd_mxfp8(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias,
+                                  1.0 / math.sqrt(H // heads), lse)
+            s1 = _lin8(st, None, st.w(L.o_w), bias=st.f32(L.o_b), resid=x, xq=oq)
+            return BertLayerFn._ffn_f8(st, L, x, s1, eps, d_out)
+        o = torch.empty_like(x)
         # the forward's dropout keep mask as bits (1 bit per score; read back by the backward)
         kbits = (N.attn_keep_bits(P, T, heads, x.device) if d_att is not None and save else None)
         N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
@@ -196,6 +246,27 @@ class BertLayerFn(torch.autograd.Function):
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
         ctx.meta = (L, P, T, heads, drops)
         ctx.kbits = kbits
+        return y
+
+    @staticmethod
+    def _ffn_f8(st, L, x, s1, eps, d_out):
+        """Eval fp8 tail of the layer: LN1 (bf16 out for the residual + MX-fp8 for FC1), FC1 ->
+        FC2 on the fp8 MFMA, LN2 (bf16 out + MX-fp8 copy for the next layer's QKV)."""
+        h1 = torch.empty_like(x)
+        m = torch.empty(s1.shape[0], device=x.device)
+        r = torch.empty_like(m)
+        if d_out is None and _f8(h1, st.w(L.i_w)) and st.w(L.out_w).shape[0] % 256 == 0:
+            h1q = _ln8(s1, st.f32(L.ln1_w), st.f32(L.ln1_b), eps, y=h1, mean=m, rstd=r)
+            s2 = _mlp_fwd(st, h1, st.w(L.i_w), st.f32(L.i_b), GELU, st.w(L.out_w), st.f32(L.out_b),
+                          h1, _linear, xq=h1q)
+        else:
+            H = x.shape[-1]
+            N.layernorm_fwd(s1.shape[0], H, s1, _rows(H), st.f32(L.ln1_w), st.f32(L.ln1_b), eps,
+                            h1, _rows(H), m, r)
+            s2 = _mlp_fwd(st, h1, st.w(L.i_w), st.f32(L.i_b), GELU, st.w(L.out_w), st.f32(L.out_b),
+                          h1, _linear)
+        y = torch.empty_like(x)
+        _ln8(s2, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=y, mean=m, rstd=r)
         return y
 
     @staticmethod
@@ -250,17 +321,31 @@ class VitBlockFn(torch.autograd.Function):
         R = h.shape[0]
         m1 = torch.empty(R, device=h.device)
         r1 = torch.empty_like(m1)
-        hn = torch.empty_like(h)
-        N.layernorm_fwd(R, W, h, _rows(W), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, hn, _rows(W),
-                        m1, r1)
-        qkv = _linear(hn, st.w(L.in_w), bias=st.f32(L.in_b))
-        o = torch.empty_like(h)
+        f8 = not save and _f8(h, st.w(L.in_w)) and _f8(h, st.w(L.fc_w))
+        if f8:  # eval, fp8 GEMMs: the LayerNorm outputs are only GEMM operands -> MX-fp8 only
+            hq = _ln8(h, st.f32(L.ln1_w), st.f32(L.ln1_b), eps, mean=m1, rstd=r1)
+            qkv = _lin8(st, None, st.w(L.in_w), bias=st.f32(L.in_b), xq=hq)
+        else:
+            hn = torch.empty_like(h)
+            N.layernorm_fwd(R, W, h, _rows(W), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, hn, _rows(W),
+                            m1, r1)
+            qkv = _linear(hn, st.w(L.in_w), bias=st.f32(L.in_b))
         lse = torch.empty(P, heads, T, device=h.device)
-        N.attn_fwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
-                   lse)
-        x1 = _linear(o, st.w(L.out_w), bias=st.f32(L.out_b), resid=h)
+        if f8:
+            oq = N.attn_fwd_mxfp8(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None,
+                                  1.0 / math.sqrt(W // heads), lse)
+            x1 = _lin8(st, None, st.w(L.out_w), bias=st.f32(L.out_b), resid=h, xq=oq)
+        else:
+            o = torch.empty_like(h)
+            N.attn_fwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o,
+                       W, lse)
+            x1 = _linear(o, st.w(L.out_w), bias=st.f32(L.out_b), resid=h)
         m2 = torch.empty_like(m1)
         r2 = torch.empty_like(m1)
+        if f8:
+            hq2 = _ln8(x1, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, mean=m2, rstd=r2)
+            return _mlp_fwd(st, None, st.w(L.fc_w), st.f32(L.fc_b), QGELU, st.w(L.proj_w),
+                            st.f32(L.proj_b), x1, _linear, xq=hq2)
         hn2 = torch.empty_like(h)
         N.layernorm_fwd(R, W, x1, _rows(W), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, hn2, _rows(W),
                         m2, r2)

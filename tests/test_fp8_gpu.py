@@ -88,7 +88,10 @@ def _exact_operand(g, rows, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 256, 512), (1000, 384, 1024),
-                                   (700, 640, 128)])  # last two: 256^2 tiles, ragged M and N
+                                   (700, 640, 128), (600, 640, 512), (2000, 1024, 1024),
+                                   (257, 300, 256)])
+# (1000, 384, 1024), (600, 640, 512), (2000, 1024, 1024), (257, 300, 256): the 256^2 8-phase F8
+# kernel (M, N >= 256, K % 256 == 0; ragged M / N); the others the 128^2 / 256^2 ring kernels
 def test_gemm_exact_operands(M, N, K):
     from multimodal_sequencing_amd import _native as N_
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
@@ -160,3 +163,72 @@ def test_gemm_mxfp8_out_matches_gemm_then_quant(rows, Nn, K, act):
     got = N.gemm_mxfp8_out(x, W, bias=b, act=act)
     assert torch.equal(got.q[:, :Nn], want.q[:, :Nn])
     assert torch.equal(got.scales, want.scales)
+
+
+@pytest.mark.parametrize("rows,Nn,K,act", [(300, 320, 256, 1), (1000, 4096, 1024, 1),
+                                           (555, 1024, 512, 2), (256, 256, 256, 0)])
+def test_gemm_mxfp8_q8_matches_gemm_then_quant(rows, Nn, K, act):
+    """fp8 GEMM with MX-fp8 output (mmseq_gemm_mxfp8_q8, FC1 -> FC2 on the fp8 MFMA) is
+    bit-identical to the fp8 GEMM's bf16 output (same activation) quantised by mmseq_quant_mxfp8."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows * 3 + Nn + K)
+    qa = N.quant_mxfp8(torch.randn(rows, K, device=DEV, generator=g).bfloat16())
+    qb = N.quant_mxfp8((torch.randn(Nn, K, device=DEV, generator=g) * 0.05).bfloat16())
+    b = torch.randn(Nn, device=DEV, generator=g) * 0.1
+    ref = torch.empty(rows, Nn, device=DEV, dtype=torch.bfloat16)
+    N.gemm_mxfp8(qa, qb, ref, bias=b, act=act)
+    want = N.quant_mxfp8(ref)
+    got = N.gemm_mxfp8_q8(qa, qb, bias=b, act=act)
+    assert torch.equal(got.q[:, :Nn], want.q[:, :Nn])
+    assert torch.equal(got.scales, want.scales)
+
+
+@pytest.mark.parametrize("rows,cols,with_y", [(300, 1024, True), (64, 768, False), (1, 256, True),
+                                              (1000, 512, True)])
+def test_layernorm_mxfp8_matches_ln_then_quant(rows, cols, with_y):
+    """LayerNorm writing MX-fp8 (mmseq_layernorm_fwd_mxfp8, the QKV / FC1 operand of the config-5
+    fp8 forward) equals the bf16 LayerNorm quantised by mmseq_quant_mxfp8: codes and packed scales
+    bit for bit (padding-row scales included), and its bf16 output equals mmseq_layernorm_fwd's."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, device=DEV, generator=g) * 3 + 1).bfloat16()
+    gamma = 1 + 0.1 * torch.randn(cols, device=DEV, generator=g)
+    beta = 0.1 * torch.randn(cols, device=DEV, generator=g)
+    y_ref = torch.empty_like(x)
+    m, r = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    N.layernorm_fwd(rows, cols, x, N.rows(cols), gamma, beta, 1e-5, y_ref, N.rows(cols), m, r)
+    want = N.quant_mxfp8(y_ref)
+    y = torch.empty_like(x) if with_y else None
+    m2, r2 = torch.empty_like(m), torch.empty_like(r)
+    got = N.layernorm_fwd_mxfp8(rows, cols, x, gamma, beta, 1e-5, y=y, mean=m2, rstd=r2)
+    assert torch.equal(got.q[:, :cols], want.q[:, :cols])
+    assert torch.equal(got.scales, want.scales)
+    if with_y:
+        assert torch.equal(y, y_ref)
+    assert torch.equal(m2, m) and torch.equal(r2, r)
+
+
+@pytest.mark.parametrize("P,T,heads,masked", [(3, 513, 2, True), (2, 393, 16, False), (1, 64, 1, False)])
+def test_attention_mxfp8_out_matches_attention_then_quant(P, T, heads, masked):
+    """The eval attention forward writing MX-fp8 (mmseq_attn_fwd_mxfp8, the output projection's
+    operand in the config-5 fp8 forward) equals the bf16 forward (same kernel) quantised by
+    mmseq_quant_mxfp8, codes and scales bit for bit, and its LSE equals the bf16 forward's."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device="cpu").manual_seed(P * T + heads)
+    H = heads * 64
+    qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, torch.bfloat16)
+    bias = None
+    if masked:
+        m = (torch.rand(P, T, generator=g) > 0.3).float()
+        m[:, 0] = 1
+        bias = ((1 - m) * -10000.0).to(DEV)
+    out = torch.empty(P * T, H, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(P, heads, T, device=DEV)
+    N.attn_set_fast(1)
+    N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, lse)
+    want = N.quant_mxfp8(out)
+    lse8 = torch.empty_like(lse)
+    got = N.attn_fwd_mxfp8(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, lse8)
+    assert torch.equal(got.q[:, :H], want.q[:, :H])
+    assert torch.equal(got.scales, want.scales)
+    assert torch.equal(lse8, lse)

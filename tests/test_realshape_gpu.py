@@ -343,14 +343,16 @@ def _rel_l2(a, b):
 
 
 # encoder-output bounds at the config-5 shape (ViT-L/14 + 1024-wide joint, 2 + 2 layers), relative
-# L2 of lang_feats (pair 0 and the last pair) against the reference's fp32 values
-C5_BOUND = {"f32": 1e-4, "bf16": 1e-2, "mxfp8": 3e-2}
+# L2 of lang_feats (pair 0 and the last pair) against the reference's fp32 values. Measured: fp32
+# 9e-7, bf16 5.4e-3, MX-fp8 3.9e-2 with all four encoder GEMMs of every layer on the fp8 MFMA
+# (round 2, FC2 only: 2.7e-2); e4m3 keeps 3 mantissa bits (2^-4 relative rounding per operand)
+C5_BOUND = {"f32": 1e-4, "bf16": 1e-2, "mxfp8": 5e-2}
 
 
 @pytest.mark.parametrize("mode", ["f32", "bf16", "mxfp8"])
 def test_config5_encoder_output_bounds(mode):
     """The benchmarked dtypes' encoder output against the reference: lang_feats relative L2 <= the
-    bound of C5_BOUND (fp32 parity 1e-4, bf16 1e-2, MX-fp8 encoder GEMMs in eval 3e-2). A broken
+    bound of C5_BOUND (fp32 parity 1e-4, bf16 1e-2, MX-fp8 encoder GEMMs in eval 5e-2). A broken
     fp8 GEMM or quantiser moves it to O(1)."""
     from multimodal_sequencing_amd import kernels as K
     meta, d, m, inputs = _config5_l2(torch.float32 if mode == "f32" else torch.bfloat16)
