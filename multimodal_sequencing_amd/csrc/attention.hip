@@ -775,12 +775,13 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
           }
         }
       }
-      mx = xlane_max4(mx);
       // lazy rescaling: the running max only moves (and O, l are rescaled) when some row's tile
       // max exceeds it by more than 8 (log2 units), so unrescaled probabilities stay <= 2^8;
-      // O / l and the LSE m + log2(l) are exact for any reference m
+      // O / l and the LSE m + log2(l) are exact for any reference m. The four lanes of a row
+      // share m, so the vote over each lane's partial max decides the same as over the row max,
+      // and the cross-lane reduction runs only when a row's max moves
       if (__ballot(mx > m[grp] + 8.f) != 0) {
-        const float mn = fmaxf(m[grp], mx);
+        const float mn = fmaxf(m[grp], xlane_max4(mx));
         const float alpha = ex2(m[grp] - mn);
         m[grp] = mn;
         lsum[grp] *= alpha;

@@ -168,9 +168,12 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
   const float inv = ldexpf(1.f, -e);
   const int Mp = (a.M + 63) & ~63;
   if (g == 0 && m < Mp && n < a.N) {
+    // through a uniform buffer descriptor and a 32-bit offset: a per-lane 64-bit pointer here is
+    // hoisted out of the tile loop, spilled, and its reload costs a vmcnt(0) per call
     const int KB = a.N >> 5;
-    a.q8_scales[((int64_t)(m >> 6) * KB + (n >> 5)) * 64 + (m & 15) * 4 + ((m >> 4) & 3)] =
-        (uint8_t)(m < a.M ? e + 127 : 0);
+    const rsrc_t rq = make_rsrc(a.q8_scales, (int64_t)(Mp >> 6) * KB * 64);
+    const uint32_t off = (uint32_t)(((m >> 6) * KB + (n >> 5)) * 64 + (m & 15) * 4 + ((m >> 4) & 3));
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(m < a.M ? e + 127 : 0), rq, off, 0, 0);
   }
   if (m >= a.M || n >= a.N) return;
   uint32_t w[2];
@@ -301,6 +304,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   const uint8_t* Ab = reinterpret_cast<const uint8_t*>(a.A);
   const uint8_t* Bb = reinterpret_cast<const uint8_t*>(a.B);
   const int KB32 = a.K >> 5;  // F8: E8M0 blocks per row
+  // LDS image order: bf16 [A0 | B0 | A1 | B1] (K-tile buffer, then operand), F8 [A0 | A1 | B0 | B1]:
+  // there every fragment read of both buffers is within the 64 KB immediate offset of one base
+  // register per (operand, k-half); with the bf16 order the F8 kernels (which hold 16 more scale
+  // and descriptor registers) spilled those bases and reloaded them inside the main loop, each
+  // reload a vmcnt(0) that waited out the in-flight DMA
+  constexpr int LBUF = F8 ? G_LDA_HALF : 2 * G_LDA_HALF;  // elements between the two buffers
+  constexpr int LOPB = F8 ? 2 * G_LDA_HALF : G_LDA_HALF;  // elements to the B image
 
   // per-lane source offsets (bytes) for a 1 KB piece = 8 rows x 128 B; the swizzle term
   // ((row >> 1) & 7) = (lane >> 4) | 4 * (g8 & 1) depends on the parity of the 8-row group
@@ -349,7 +359,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     const bool isA = (X == 0 || X == 3);
     const rsrc_t r = isA ? (nxt ? rAn : rAc) : (nxt ? rBn : rBc);
     const int64_t ld = isA ? lda_b : ldb_b;
-    unsigned short* img = smem + (kk & 1) * (2 * G_LDA_HALF) + (isA ? 0 : G_LDA_HALF);
+    unsigned short* img = smem + (kk & 1) * LBUF + (isA ? 0 : LOPB);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = wave * 2 + i;
@@ -381,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   const int hb = ((l15 >> 1) & 1) | ((l15 >> 2) << 1);
   const int swb0 = ((lane >> 4) ^ hb) << 3;
   const int swb1 = ((4 + (lane >> 4)) ^ hb) << 3;
-  const int brow = G_LDA_HALF + ((wc >> 1) * 128 + (wc & 1) * 64 + 8 * (l15 >> 2) + (l15 & 3)) * 64;
+  const int brow = LOPB + ((wc >> 1) * 128 + (wc & 1) * 64 + 8 * (l15 >> 2) + (l15 & 3)) * 64;
 #define FR(base, t, ks) __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>( \
       smem + (base) + (t) * 1024 + ((ks) ? sw1 : sw0)))
 #define FRB(base, j, ks) __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>( \
@@ -451,7 +461,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     for (int s = 0; s < (nk >> 1); ++s) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // h = 0: even K-tile 2s, h = 1: odd K-tile 2s + 1
-        const int buf = h * (2 * G_LDA_HALF);
+        const int buf = h * LBUF;
         // ---- phase 1 (5): A_lo + B_lo, quadrant (i 0-3, j 0-1)
 #pragma unroll
         for (int i = 0; i < 4; ++i) LDA(i);
@@ -513,7 +523,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     int tm, tn;
     tile_mn(tile, tiles_n, ntiles, tm, tn);
     const int m0 = tm * 256, n0 = tn * 256;
-    const int g = lane >> 4, ii = lane & 15;
+    // Q8: the lane index re-read per tile (volatile asm), so the epilogue's lane-derived offsets
+    // are recomputed here instead of hoisted out of the tile loop, spilled and reloaded
+    int lane_e = lane;
+    if (Q8) asm volatile("v_mov_b32 %0, %1" : "=v"(lane_e) : "v"(lane));
+    const int g = lane_e >> 4, ii = lane_e & 15;
     if (ACT < 0) {  // benchmark-only variant: main loop without the epilogue stores
 #pragma unroll
       for (int i = 0; i < 8; ++i)

@@ -56,14 +56,16 @@ def test_abi_exports_every_declared_symbol():
     assert lib.mmseq_version().startswith(b"mmseq")
 
 
-def test_code_object_m0_only_feeds_lds_dma():
-    """The LDS-DMA helper (csrc/gemm_common.h dma16) writes m0 from inline asm, which the compiler
-    does not track: check in the built gfx950 code object that every m0 write is that helper's
-    `s_mov_b32 m0, sN` directly followed by its `buffer_load_dwordx4 ... lds`, and that nothing
-    compiler-generated reads m0 (indexed moves, messages, GWS, interpolation)."""
+_DISASM = []
+
+
+def _disasm():
+    """llvm-objdump -d of the gfx950 code object inside the built library (cached)."""
     import shutil
     import subprocess
     import tempfile
+    if _DISASM:
+        return _DISASM[0]
     llvm = "/opt/rocm/lib/llvm/bin"
     if not (shutil.which("objcopy") and os.path.exists(os.path.join(llvm, "llvm-objdump"))):
         pytest.skip("objcopy / ROCm llvm tools not available")
@@ -74,19 +76,65 @@ def test_code_object_m0_only_feeds_lds_dma():
         # the library under every process that has it mapped (SIGBUS later in this process)
         subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", so,
                         os.path.join(d, "copy.so")], check=True)
-        subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--type=o", f"--input={fb}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}", "--unbundle"],
-                       check=True)
-        asm = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", "--mcpu=gfx950", co],
-                             check=True, capture_output=True, text=True).stdout
+        # one offload bundle per translation unit, concatenated: unbundle each
+        data = open(fb, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+        assert starts and starts[0] == 0
+        asm = ""
+        for k, st in enumerate(starts):
+            part = os.path.join(d, f"b{k}.bin")
+            with open(part, "wb") as f:
+                f.write(data[st:starts[k + 1] if k + 1 < len(starts) else len(data)])
+            subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--type=o",
+                            f"--input={part}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                            f"--output={co}", "--unbundle"], check=True)
+            asm += subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", "--mcpu=gfx950", co],
+                                  check=True, capture_output=True, text=True).stdout
+    _DISASM.append(asm)
+    return asm
+
+
+def test_code_object_m0_only_feeds_lds_dma():
+    """The LDS-DMA helper (csrc/gemm_common.h dma16) writes m0 from inline asm, which the compiler
+    does not track: check in the built gfx950 code object that every m0 write is that helper's
+    `s_mov_b32 m0, sN` directly followed by its `buffer_load_dwordx4 ... lds`, and that nothing
+    compiler-generated reads m0 (indexed moves, messages, GWS, interpolation)."""
+    asm = _disasm()
     lines = [l.split("//")[0].strip() for l in asm.splitlines()]
     lines = [l for l in lines if l and not l.endswith(">:")]
     writes = 0
     for k, l in enumerate(lines):
         if re.search(r"\bm0\b", l):
-            assert re.fullmatch(r"s_mov_b32 m0, s\d+", l), l
+            assert re.fullmatch(r"s_mov_b32 m0, (s\d+|vcc_lo|vcc_hi)", l), l
             assert lines[k + 1].startswith("buffer_load_dwordx4") and lines[k + 1].endswith("lds"), \
                 lines[k + 1]
             writes += 1
         assert not re.match(r"(s_movrel|v_movrel|s_sendmsg|ds_gws|s_set_gpr_idx|v_interp)", l), l
     assert writes > 0
+
+
+def test_fp8_gemm_kernels_do_not_spill():
+    """The MX-fp8 instantiations of the 256 x 256 NT GEMM (gemm256.hip F8, with and without the
+    MX-fp8 epilogue Q8) keep every value in registers: a scratch reload in that kernel is a
+    vmcnt(0) (scratch counts in vmcnt, which retires in order) that waits out the in-flight
+    LDS-DMA of the K-loop or the stores of the epilogue. The bf16 instantiations the training step
+    runs (plain, residual, GELU / QuickGELU forward and dgrad) are held to the same rule."""
+    asm = _disasm()
+    kern, seen, bad = None, set(), {}
+    for l in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:", l)
+        if m:
+            kern = m.group(1)
+            continue
+        if kern and "gemm256_nt_kernel" in kern:
+            seen.add(kern)
+            if "scratch_" in l.split("//")[0]:
+                bad[kern] = bad.get(kern, 0) + 1
+    f8 = [k for k in seen if re.search(r"ELb1EEEvN17mmseq_gemm_detail", k)]
+    assert len(f8) >= 9, sorted(seen)
+    hot = [k for k in seen if re.search(r"gemm256_nt_kernelILi[012]ELb(0ELb0|1ELb1|0ELb1)ELb0ELb0E", k)
+           and "ILi1ELb0ELb1" not in k and "ILi2ELb0ELb1" not in k]
+    assert len(hot) >= 6, sorted(seen)
+    offenders = {k: n for k, n in bad.items() if k in f8 or k in hot}
+    assert not offenders, offenders

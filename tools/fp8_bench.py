@@ -41,7 +41,9 @@ def main():
         t_q = timeit(lambda: N.quant_mxfp8(A, out=qa))
         t_fp8 = timeit(lambda: N.gemm_mxfp8(qa, qw, C, bias=bias, act=act))
         fl = 2.0 * M * Nn * K
+        t_q8 = timeit(lambda: N.gemm_mxfp8_q8(qa, qw, bias=bias, act=act)) if Nn >= 3072 else None
         out["shapes"].append({"gemm": name, "N": Nn, "K": K,
+                              "mxfp8_q8out_us": t_q8 * 1e6 if t_q8 else None,
                               "bf16_us": t_bf16 * 1e6, "bf16_tflops": fl / t_bf16 / 1e12,
                               "mxfp8_us": t_fp8 * 1e6, "mxfp8_tflops": fl / t_fp8 / 1e12,
                               "quant_act_us": t_q * 1e6,
