@@ -588,6 +588,18 @@ __device__ __forceinline__ rsrc_t head_rsrc(const void* base, int64_t row0, int6
   return make_rsrc(b, ((int64_t)(T - 1) * ld + 64) * 2);
 }
 
+// Prologue loads through buffer descriptors: rows / indices past the descriptor's range read as
+// zero without a branch, so the compiler issues every prologue load straight-line and waits once
+// (a bounds branch around a load gets its own wait at the branch's first use)
+__device__ __forceinline__ bf16x8_t buf_row_frag(rsrc_t r, int row, int64_t ld, int ks, int lane) {
+  typedef unsigned int u32x4b __attribute__((ext_vector_type(4)));
+  const uint32_t off = (uint32_t)(((int64_t)row * ld + ks * 32 + (lane >> 4) * 8) * 2);
+  return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float buf_f32(rsrc_t r, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)idx * 4u, 0, 0));
+}
+
 // 1-D grid over (row block, head, pair) with an XCD-aware order: the blocks that share one
 // (pair, head) K/V (or Q/dO) slice get consecutive work indices on ONE XCD (blocks b, b+8, ...
 // share an XCD under round-robin dispatch), so the slice is fetched into that XCD's L2 once.
@@ -669,25 +681,35 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
     }
   };
   stage(0);
+  // the prologue's global loads (this wave's key-bias tiles for T <= 1024, the Q fragments) are
+  // all issued before the first is consumed: one memory round trip beside tile 0's DMA
   const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
   int* sZero = reinterpret_cast<int*>(sBias + nkt * 64);  // tile t's key bias is all zero
-  for (int tt = wave; tt < nkt; tt += 4) {
-    const int k = tt * 64 + lane;
-    const float bv = k < T ? (kbias ? kbias[k] * LOG2E : 0.f) : -1e30f;
-    sBias[k] = bv;
-    const bool z = __ballot(bv != 0.f) == 0;
-    if (lane == 0) sZero[tt] = z;
-  }
-  const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
-                             a.q_off + h * 64;
+  const rsrc_t rkb = make_rsrc(kbias, kbias ? (int64_t)T * 4 : 0);
+  float kbv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) kbv[j] = buf_f32(rkb, (wave + 4 * j) * 64 + lane);
+  const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
   bf16x8_t qf[2][2];
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      qf[grp][ks] = glob_row_frag(Qb, ld, qw + grp * 16 + i, T, ks, lane);
-      settle(qf[grp][ks]);
-    }
+    for (int ks = 0; ks < 2; ++ks) qf[grp][ks] = buf_row_frag(rq, qw + grp * 16 + i, ld, ks, lane);
+  auto put_bias = [&](int tt, float raw) {
+    const int k = tt * 64 + lane;
+    const float bv = k < T ? raw * LOG2E : -1e30f;
+    sBias[k] = bv;
+    const bool z = __ballot(bv != 0.f) == 0;
+    if (lane == 0) sZero[tt] = z;
+  };
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (wave + 4 * j < nkt) put_bias(wave + 4 * j, kbv[j]);
+  for (int tt = wave + 16; tt < nkt; tt += 4) put_bias(tt, buf_f32(rkb, tt * 64 + lane));
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) settle(qf[grp][ks]);
 
   const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
   int to[4];
@@ -1238,27 +1260,49 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     }
   };
   stage(0);
+  // the prologue's global loads (key bias for T <= 1024, Q / dO / O fragments, LSE) are all issued
+  // before the first is consumed: one memory round trip beside tile 0's DMA
   const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
-  for (int k = tid; k < nkt * 64; k += 256)
-    sBias[k] = k < T ? (kbias ? kbias[k] * LOG2E : 0.f) : -1e30f;
+  const rsrc_t rkb = make_rsrc(kbias, kbias ? (int64_t)T * 4 : 0);
+  float kbv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) kbv[j] = buf_f32(rkb, tid + 256 * j);
   const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
                              a.q_off + h * 64;
   const unsigned short* dOb = reinterpret_cast<const unsigned short*>(a.dout) +
                               (int64_t)p * T * a.ld_dout + h * 64;
   const unsigned short* Ob = reinterpret_cast<const unsigned short*>(a.out) +
                              (int64_t)p * T * a.ld_out + h * 64;
-  bf16x8_t qf[2][2], of[2][2];
+  bf16x8_t qf[2][2], of[2][2], ovf[2][2];
   float L2[2], Dd[2];
+  const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
+  const rsrc_t rdo = head_rsrc(a.dout, (int64_t)p * T, a.ld_dout, h * 64, T);
+  const rsrc_t rout = head_rsrc(a.out, (int64_t)p * T, a.ld_out, h * 64, T);
+  const rsrc_t rlse = make_rsrc(a.lse + ((int64_t)p * a.heads + h) * T, (int64_t)T * 4);
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int q = qw + grp * 16 + i;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[grp][ks] = buf_row_frag(rq, q, ld, ks, lane);
+      of[grp][ks] = buf_row_frag(rdo, q, a.ld_dout, ks, lane);
+      ovf[grp][ks] = buf_row_frag(rout, q, a.ld_out, ks, lane);
+    }
+    L2[grp] = buf_f32(rlse, q);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = tid + 256 * j;
+    if (k < nkt * 64) sBias[k] = k < T ? kbv[j] * LOG2E : -1e30f;
+  }
+  for (int k = tid + 1024; k < nkt * 64; k += 256) sBias[k] = k < T ? buf_f32(rkb, k) * LOG2E : -1e30f;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
     const int q = qw + grp * 16 + i;
     float dot = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      qf[grp][ks] = glob_row_frag(Qb, ld, q, T, ks, lane);
-      of[grp][ks] = glob_row_frag(dOb, a.ld_dout, q, T, ks, lane);
-      const bf16x8_t ov = glob_row_frag(Ob, a.ld_out, q, T, ks, lane);
-      const u16x8 x = __builtin_bit_cast(u16x8, of[grp][ks]), y = __builtin_bit_cast(u16x8, ov);
+      const u16x8 x = __builtin_bit_cast(u16x8, of[grp][ks]), y = __builtin_bit_cast(u16x8, ovf[grp][ks]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) dot = fmaf(bf2f(x[e]), bf2f(y[e]), dot);
     }
@@ -1266,7 +1310,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     dot += __shfl_xor(dot, 32, 64);
     Dd[grp] = dot;
     const int64_t ri = ((int64_t)p * a.heads + h) * T + q;
-    L2[grp] = q < T ? a.lse[ri] * LOG2E : 1e30f;
+    L2[grp] = q < T ? L2[grp] * LOG2E : 1e30f;
     if (q < T && g == 0) a.delta[ri] = dot;
     settle(qf[grp][0]);
     settle(qf[grp][1]);
@@ -1424,27 +1468,64 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
             (uint32_t)((((int64_t)(t * 64 + lane)) * a.nkt2 + kt0 + 2) * 8));
   };
   stage(0);
+  // the prologue's global loads (LSE / delta rows for T <= 1024, the key and value fragments, the
+  // key bias, the tail keys) are all issued before the first is consumed: one memory round trip
+  // (beside tile 0's DMA) instead of one per loop iteration and fragment group
   const int64_t rb = ((int64_t)p * a.heads + h) * T;
-  for (int q = tid; q < nqt * 64; q += 256) {
-    sL[q] = q < T ? a.lse[rb + q] * LOG2E : 1e30f;  // exp2(x - 1e30) = 0 for padded queries
-    sD[q] = q < T ? a.delta[rb + q] : 0.f;
+  const rsrc_t rlse = make_rsrc(a.lse + rb, (int64_t)T * 4), rdel = make_rsrc(a.delta + rb, (int64_t)T * 4);
+  float lv[4], dlv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lv[j] = buf_f32(rlse, tid + 256 * j);
+    dlv[j] = buf_f32(rdel, tid + 256 * j);
   }
-  const unsigned short* Kb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
-                             a.k_off + h * 64;
-  const unsigned short* Vb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
-                             a.v_off + h * 64;
+  const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
+  const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
+  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+  const rsrc_t rkb = make_rsrc(kbias, kbias ? (int64_t)T * 4 : 0);
   bf16x8_t kf[2][2], vf[2][2];
   float kb2[2];
-  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
     const int key = kw + grp * 16 + i;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      kf[grp][ks] = glob_row_frag(Kb, ld, key, T, ks, lane);
-      vf[grp][ks] = glob_row_frag(Vb, ld, key, T, ks, lane);
+      kf[grp][ks] = buf_row_frag(rk, key, ld, ks, lane);
+      vf[grp][ks] = buf_row_frag(rv, key, ld, ks, lane);
     }
-    kb2[grp] = key < T ? (kbias ? kbias[key] * LOG2E : 0.f) : -1e30f;
+    kb2[grp] = buf_f32(rkb, key);
+  }
+  float kb2t = 0.f;
+  u16x8 kvt[4];
+  if (tailb) {  // block-uniform
+    const int key = a.tail0 + i;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kvt[ks] = __builtin_bit_cast(u16x8, buf_row_frag(rk, key, ld, ks, lane));
+      kvt[2 + ks] = __builtin_bit_cast(u16x8, buf_row_frag(rv, key, ld, ks, lane));
+    }
+    kb2t = buf_f32(rkb, key);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = tid + 256 * j;
+    if (q < nqt * 64) {
+      sL[q] = q < T ? lv[j] * LOG2E : 1e30f;  // exp2(x - 1e30) = 0 for padded queries
+      sD[q] = q < T ? dlv[j] : 0.f;
+    }
+  }
+  for (int q = tid + 1024; q < nqt * 64; q += 256) {
+    sL[q] = q < T ? buf_f32(rlse, q) * LOG2E : 1e30f;
+    sD[q] = q < T ? buf_f32(rdel, q) : 0.f;
+  }
+  if (tailb && wave == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sKVt[e * 64 + lane] = kvt[e];
+  }
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int key = kw + grp * 16 + i;
+    kb2[grp] = key < T ? kb2[grp] * LOG2E : -1e30f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       settle(kf[grp][ks]);
@@ -1452,18 +1533,11 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     }
     settle(kb2[grp]);
   }
-  float kb2t = -1e30f;
   if (tailb) {
-    const int key = a.tail0 + i;
-    if (wave == 0) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        sKVt[ks * 64 + lane] = __builtin_bit_cast(u16x8, glob_row_frag(Kb, ld, key, T, ks, lane));
-        sKVt[(2 + ks) * 64 + lane] = __builtin_bit_cast(u16x8, glob_row_frag(Vb, ld, key, T, ks, lane));
-      }
-    }
-    kb2t = key < T ? (kbias ? kbias[key] * LOG2E : 0.f) : -1e30f;
+    kb2t = a.tail0 + i < T ? kb2t * LOG2E : -1e30f;
     settle(kb2t);
+  } else {
+    kb2t = -1e30f;
   }
   const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
   int to[4];
