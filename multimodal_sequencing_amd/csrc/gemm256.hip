@@ -280,8 +280,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   // 128 KB of K-tile buffers, then (dgrad variants) the 13 KB activation-derivative table or (F8)
   // the 2 x 2 KB scale buffers
   __shared__ __attribute__((aligned(16))) unsigned short
-      smem[2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0) + (F8 ? 2048 : 0)];
+      smem[2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0) + (F8 ? 2048 : 0) + 1024];
   unsigned short* const sscale = smem + 2 * 2 * G_LDA_HALF;  // F8: [2 buffers][A 1 KB | B 1 KB]
+  // the tile's 256 bias values, [2 tiles][1 KB]: DMA'd by wave 0 before the tile's K-loop (older
+  // than the first iteration's stages, so retired by its phase-4 counted wait and visible after
+  // that phase's barrier), read by the epilogue from LDS. A global bias load in the epilogue was
+  // its first wait, a vmcnt(0) (the compiler cannot see the in-flight LDS-DMA of the next tile's
+  // first K-tiles, and that wait drained them).
+  unsigned short* const sbias = smem + 2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0) + (F8 ? 2048 : 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -328,6 +334,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   // F8: the scale arrays (one descriptor each for the whole kernel) and the first 64-row scale
   // group of a tile's A / B rows; past the last tile, groups whose offsets fall outside the array
   // (zero-fill, no traffic)
+  const rsrc_t rBias = make_rsrc(a.bias, a.bias ? (int64_t)a.N * 4 : 0);  // columns >= N read 0
   const rsrc_t rSA = make_rsrc(a.f8_sa, F8 ? a.f8_sa_bytes : 0);
   const rsrc_t rSB = make_rsrc(a.f8_sb, F8 ? a.f8_sb_bytes : 0);
   struct Sc { int ga, gb; };
@@ -457,6 +464,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (ACT >= 0 && wave == 0) {
+      uint32_t ln;  // the lane index recomputed here (not a hoisted, possibly spilled lane constant)
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      dma16(rBias, sbias + (it & 1) * 512, (uint32_t)(scc.gb * 256) + ln * 16u);
+    }
 
     for (int s = 0; s < (nk >> 1); ++s) {
 #pragma unroll
@@ -539,7 +551,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
       descs(tile + 2 * G, rAn, rBn, scn);
       continue;
     }
-    const EpiBias bias0 = epi_bias(a, n0 + wc * 64 + 8 * g), bias1 = epi_bias(a, n0 + wc * 64 + 32 + 8 * g);
+    EpiBias bias0, bias1;
+    {
+      const float* sb = reinterpret_cast<const float*>(sbias + (it & 1) * 512) + wc * 64 + 8 * g;
+      bias0.b0 = *reinterpret_cast<const f32x4*>(sb);
+      bias0.b1 = *reinterpret_cast<const f32x4*>(sb + 4);
+      bias1.b0 = *reinterpret_cast<const f32x4*>(sb + 32);
+      bias1.b1 = *reinterpret_cast<const f32x4*>(sb + 36);
+    }
     if (XIN) {
       // batches of 4 calls; the operand loads of batch h + 1 are issued before the stores of batch
       // h, and each batch is consumed (settled) once, so its wait never covers a store (vmcnt

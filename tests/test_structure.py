@@ -131,8 +131,10 @@ def test_fp8_gemm_kernels_do_not_spill():
             seen.add(kern)
             if "scratch_" in l.split("//")[0]:
                 bad[kern] = bad.get(kern, 0) + 1
-    f8 = [k for k in seen if re.search(r"ELb1EEEvN17mmseq_gemm_detail", k)]
-    assert len(f8) >= 9, sorted(seen)
+    # (the forward GELU / QuickGELU + residual instantiations, ILi[12]ELb0ELb1, have no caller)
+    f8 = [k for k in seen if re.search(r"ELb1EEEvN17mmseq_gemm_detail", k)
+          and not re.search(r"ILi[12]ELb0ELb1", k)]
+    assert len(f8) >= 7, sorted(seen)
     hot = [k for k in seen if re.search(r"gemm256_nt_kernelILi[012]ELb(0ELb0|1ELb1|0ELb1)ELb0ELb0E", k)
            and "ILi1ELb0ELb1" not in k and "ILi2ELb0ELb1" not in k]
     assert len(hot) >= 6, sorted(seen)
