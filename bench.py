@@ -492,11 +492,32 @@ def main():
                 dist.barrier()
             torch.cuda.synchronize()
             fwd_dt = time.perf_counter() - f0
+            floss = {"bf16": float(model(fbs[0])[0])}
+            # the same forward with the MX-fp8 encoder GEMMs (kernels.fp8_forward: QKV, O, FC1, FC2
+            # of every ViT block and joint layer on v_mfma_scale_f32_16x16x128_f8f6f4); the
+            # first pass quantises the weights
+            with K.fp8_forward(True):
+                for b in fbs:
+                    model(b)
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                f0 = time.perf_counter()
+                for _ in range(args.fwd_steps):
+                    for b in fbs:
+                        model(b)
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                fwd8_dt = time.perf_counter() - f0
+                floss["mxfp8"] = float(model(fbs[0])[0])
         model.train()
         if world > 1:
-            t = torch.tensor([fwd_dt], device=dev)
+            t = torch.tensor([fwd_dt, fwd8_dt], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            fwd_dt = t.item()
+            fwd_dt, fwd8_dt = t[0].item(), t[1].item()
 
     Nst, per = preset["N"], preset["per_seq"]
     Pst = Nst * (Nst - 1)
@@ -547,6 +568,13 @@ def main():
                           "mfma_frac_of_measured_peak": (fst * fwd / 1e12 / mpk) if mpk else None,
                           "mode": "eval (no dropout), torch.no_grad, full model forward incl. "
                                   "BERSON head + loss; ViT + joint encoder are >99.9% of FLOPs"}
+        f8 = args.batch * args.fwd_steps * world / fwd8_dt
+        out["forward"]["mxfp8"] = {
+            "stories_per_s": f8, "tflops": f8 * fwd / 1e12, "speedup_vs_bf16": f8 / fst,
+            "loss_bf16": floss["bf16"], "loss_mxfp8": floss["mxfp8"],
+            "loss_rel_diff": abs(floss["mxfp8"] - floss["bf16"]) / max(1e-12, abs(floss["bf16"])),
+            "mode": "the same forward under kernels.fp8_forward(): the four encoder GEMMs of every "
+                    "ViT block and joint layer on the MX-fp8 MFMA (tests/test_fp8_gpu.py)"}
     gs = timer.summary()
     if gs:
         traffic, tsrc = pmc_traffic()
