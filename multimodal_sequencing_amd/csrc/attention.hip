@@ -1662,7 +1662,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
       dpt = mma(o1, __builtin_bit_cast(bf16x8_t, sKVt[192 + lane]), dpt);
       const f32x4 Lq = *reinterpret_cast<const f32x4*>(sL + t * 64 + qs * 16 + 4 * g);
       const f32x4 Dq = *reinterpret_cast<const f32x4*>(sD + t * 64 + qs * 16 + 4 * g);
-      // DMODE 2: tail key j = i of its tile: bit ((i >> 2) & 3) * 16 + (i & 3), dword (i >> 3) & 1
+      // DMODE 2: tail key j = i of its tile: bit ((i >> 2) & 1) * 16 + (i & 3), dword (i >> 3) & 1
       const uint32_t* bwt = reinterpret_cast<const uint32_t*>(sBitsT + (t & 1) * 512) + ((i >> 3) & 1);
       const uint32_t post = ((i >> 2) & 1) * 16 + (i & 3);
       const uint64_t dbt = (uint64_t)(rb + t * 64 + qs * 16 + 4 * g) * (uint64_t)Tp2 + a.tail0 + i;

@@ -204,10 +204,13 @@ class GradAllReduce:
     count as complete when the first unit of another store reports a backward begin (the BERSON
     head: autograd runs all of its nodes before the inner model's last layer). Only the last
     micro-batch's backward is armed; finish() issues what is left and waits for every bucket.
+    `force=True` arms the reducer at world size 1 as well (an initialised group is required), so
+    that the RCCL path runs end to end on a one-GPU box.
     """
 
-    def __init__(self, stores, bucket_mb=64, units=None, begin_units=(), group=None):
+    def __init__(self, stores, bucket_mb=64, units=None, begin_units=(), group=None, force=False):
         self.stores = list(stores)
+        self.force = bool(force)
         self.cap = max(1, int(bucket_mb * (1 << 20)) // 4)
         self.group = group
         self.armed = False
@@ -267,7 +270,7 @@ class GradAllReduce:
 
     def arm(self, on):
         """Arm (last micro-batch) or disarm the backward-driven all-reduce."""
-        self.armed = bool(on) and self._world() > 1
+        self.armed = bool(on) and (self._world() > 1 or self.force)
         if self.armed:
             self.works = []
             for s in self.stores:
@@ -309,7 +312,7 @@ class GradAllReduce:
     def finish(self):
         """Issue every bucket not yet issued and wait for all (grads are the mean afterwards)."""
         world = self._world()
-        if world == 1:
+        if world == 1 and not self.force:
             return
         if not self.armed:
             self.arm(True)

@@ -11,6 +11,10 @@ mode "real":    GPU (every rank on cuda:0, gloo): the product model (fp32, eval)
                 final local gradient from an unarmed backward of the same story (a bucket that
                 fired before its gradients were final differs); rank 0 also runs the
                 single-process step over all the ranks' stories for the parent to compare.
+mode "rccl":    GPU, backend "nccl" (= RCCL) at world size 1 on the box's one GPU: a bucket-sized
+                all_reduce(AVG), then the product model's real backward with the reducer forced
+                on (GradAllReduce(force=True)), so _fire / finish run their RCCL branch
+                (ReduceOp.AVG, no host-side division) end to end.
 """
 import json
 import os
@@ -176,11 +180,50 @@ def real(out, rank):
         json.dump(res, f)
 
 
+def rccl(out, rank):
+    from multimodal_sequencing_amd import model_zoo
+    dev = torch.device("cuda", 0)
+    res = {"backend": dist.get_backend(), "world": dist.get_world_size(),
+           "rccl_version": ".".join(str(v) for v in torch.cuda.nccl.version())}
+    # a 64 MB bucket (the reducer's default cap) through all_reduce(AVG)
+    x = torch.randn(16 << 20, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    want = x.clone()
+    dist.all_reduce(x, op=dist.ReduceOp.AVG)
+    torch.cuda.synchronize()
+    res["avg_bucket_equal"] = bool(torch.equal(x, want))
+    # the product model's backward with the RCCL reducer armed at world 1
+    m = model_zoo.build_from_golden(REAL_CFG, device=dev)
+    m.eval()
+    stores = m.stores()
+    mine = {k: v[:1] for k, v in real_inputs(1).items()}
+    m.zero_grad()
+    m(mine)[0].backward()
+    torch.cuda.synchronize()
+    local = [s.grad.clone() for s in stores]
+    units, begin = m.ddp_units()
+    red = GradAllReduce(stores, bucket_mb=0.05, units=units, begin_units=begin, force=True)
+    m.zero_grad()
+    red.arm(True)
+    res["armed"] = red.armed
+    m(mine)[0].backward()
+    res["fired_in_backward"] = len(red.works)
+    res["avg_ops"] = sum(1 for _, _, avg in red.works if avg)
+    red.finish()
+    torch.cuda.synchronize()
+    res["buckets"] = sum(len(red.plan[id(s)]["buckets"]) for s in stores)
+    res["max_rel_diff"] = max(float((s.grad - g).abs().max()) / (float(g.abs().max()) + 1e-30)
+                              for s, g in zip(stores, local))
+    with open(os.path.join(out, f"rccl{rank}.json"), "w") as f:
+        json.dump(res, f)
+
+
 def main():
     out, mode = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "flat")
-    dist.init_process_group("gloo")
+    if mode == "rccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group("nccl" if mode == "rccl" else "gloo")
     rank = dist.get_rank()
-    {"flat": flat, "overlap": overlap, "real": real}[mode](out, rank)
+    {"flat": flat, "overlap": overlap, "real": real, "rccl": rccl}[mode](out, rank)
     dist.destroy_process_group()
 
 

@@ -52,3 +52,23 @@ def test_dp_reducer_real_backward_two_ranks(tmp_path):
         torch.testing.assert_close(g0, (res[0]["local"][i] + res[1]["local"][i]) / 2,
                                    rtol=1e-5, atol=1e-6 * scale)
         torch.testing.assert_close(g0, single[i], rtol=1e-5, atol=1e-6 * scale)
+
+
+def test_rccl_reducer_world1(tmp_path):
+    """The reducer's RCCL branch (ReduceOp.AVG, trainer.py GradAllReduce._fire) executed on the
+    box's GPU: backend "nccl" at world size 1 (RCCL refuses two ranks on one GPU), the reducer
+    forced on, buckets issued during the real backward and finished; at world 1 the mean is the
+    local gradient (float-atomic rounding aside)."""
+    port = 29500 + (os.getpid() * 17 + 7) % 2000
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                    "--nproc-per-node=1", "--master-addr", "127.0.0.1", "--master-port",
+                    str(port), os.path.join(HERE, "dist_worker.py"), str(tmp_path), "rccl"],
+                   check=True, timeout=240, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    it = json.load(open(tmp_path / "rccl0.json"))
+    print(f"RCCL {it['rccl_version']}: backend {it['backend']}, {it['buckets']} buckets, "
+          f"{it['fired_in_backward']} issued during the backward ({it['avg_ops']} AVG)")
+    assert it["backend"] == "nccl" and it["world"] == 1
+    assert it["avg_bucket_equal"]
+    assert it["armed"] and it["fired_in_backward"] >= 10
+    assert it["avg_ops"] == it["fired_in_backward"]  # the RCCL AVG branch, not gloo's SUM + div
+    assert it["max_rel_diff"] <= 1e-5, it

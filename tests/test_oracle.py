@@ -97,3 +97,22 @@ def test_oracle_real_config3_story():
         if k.startswith("gn::"):
             g = params[k[4:]].grad
             assert abs(float(g.double().norm()) - float(d[k])) <= 1e-4 * float(d[k]) + 1e-6, k
+
+
+def test_bf16_emulation_without_rounding_is_the_oracle():
+    """tests/bf16_emulation.py (the checker of tests/test_bf16_drift_gpu.py) restates the oracle's
+    encoder: with no rounding site it reproduces the oracle bit for bit, and with every site its
+    drift is of bf16's size."""
+    import bf16_emulation as E
+    meta, d, p = load_fixture("tiny")
+    cfg = oracle_cfg(meta)
+    pair = O.prepare_berson_inputs(d["input_ids"], d["labels"], cfg["N"])
+    img = torch.from_numpy(d["images"])
+    with torch.no_grad():
+        ref = O.encode(p, pair, img, cfg)
+        same = E.encode(p, pair, img, cfg, ())
+        r16 = E.encode(p, pair, img, cfg, E.ALL)
+    for k in ("lang", "okey", "clean"):
+        assert torch.equal(ref[k], same[k]), k
+    drift = float((r16["lang"] - ref["lang"]).norm() / ref["lang"].norm())
+    assert 1e-3 < drift < 2e-2, drift

@@ -8,12 +8,16 @@ worst and three more orders match the reference's (north_star 1e-4 on the loss =
 bf16 perf mode (the benchmarked dtype): the bf16 error of the MARGIN (second-best minus best
 NLL, bf16 model vs the reference's) is measured per story; where the margin exceeds DECISIVE x
 that error the bf16 beam order must equal the reference's EXACTLY; the others are reported as
-near-ties. The fixtures were made so that the check cannot be vacuous (tools/decisive_probe.py):
-each fixture must have a decisive story, so a bf16 regression that moves the margins fails the test
-either way. At config 3 the bf16 margin error is 0.01-0.8 nats on margins of 0.3-4 nats (24
-encoder layers of bf16 rounding reach the pointer logits): which of its 4 stories are decisive moves
-with any rounding change of the build (one story measured 0.12-1.4 nats of error over four
-builds), so the fixture holds 4 stories and the check asks for at least one.
+near-ties; at least half of every fixture's stories must be decisive, so a bf16 regression that
+moves the margins fails the test either way (fixture scalings picked with tools/decisive_probe.py).
+
+Where the bf16 margin error comes from (tests/bf16_placement_probe.py, profiles/r4_bf16_placement.log):
+the product's full-depth drift equals that of an ideal bf16 placement of the same roundings
+(tests/bf16_emulation.py; lang_feats 1.18e-2 both), and with the fixtures' fp32 counter weights the
+dominant term is the bf16 rounding of the WEIGHT operands — a systematic perturbation of the
+model that the span pooling does not average out (pointer keys 3.5e-3 relative from it alone; all
+the activation roundings together give 1e-3). `decisive_config3_bf16w` holds 8 stories whose
+weights are bf16-representable, so there the margin error measures the activation arithmetic alone.
 """
 import json
 import os
@@ -27,7 +31,7 @@ from golden_util import GOLDEN
 from make_golden_real import real_inputs, scale_decisive
 
 pytestmark = pytest.mark.gpu
-FIXTURES = ["decisive_tiny", "decisive_config3"]
+FIXTURES = ["decisive_tiny", "decisive_config3", "decisive_config3_bf16w"]
 
 if torch.cuda.is_available():
     from multimodal_sequencing_amd import model_zoo
@@ -89,8 +93,9 @@ def test_decisive_order_fp32(name):
 def test_decisive_order_bf16_exact(name):
     meta, d = _load(name)
     m = _model(name, meta, torch.bfloat16)
-    decisive = 0
+    decisive = n = 0
     for b, inp in _stories(meta):
+        n += 1
         ref = [int(x) for x in d["order"][b]]
         srt = np.argsort(d["perm_nll"][b])
         best, second = int(srt[0]), int(srt[1])
@@ -104,4 +109,4 @@ def test_decisive_order_bf16_exact(name):
         if margin > DECISIVE * err:
             decisive += 1
             assert order == ref, (name, b, order, ref, margin, err)
-    assert decisive >= 1, (name, decisive)  # the check is not vacuous
+    assert decisive >= (n + 1) // 2, (name, decisive, n)  # the check is not vacuous

@@ -146,6 +146,20 @@ def test_config3_story_bf16_close_to_reference():
         assert abs(gap) < 5e-3, (order, ref_order, gap)
 
 
+# full-depth (12 ViT blocks + 12 joint layers) encoder output of the config-3 story against the
+# reference: relative L2 of lang_feats (pair 0 and pair 19), the tensor the BERSON head reads
+C3_BOUND = {"f32": 1e-4, "bf16": 1.5e-2}  # measured 1.5e-6 / 1.17e-2 (24 layers)
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_config3_encoder_output_bounds(mode):
+    meta, d, m, inputs = _config3(torch.float32 if mode == "f32" else torch.bfloat16)
+    lang = _lang_feats(m, inputs).cpu().numpy()
+    errs = [_rel_l2(lang[0], d["i::lang_feats_p0"]), _rel_l2(lang[19], d["i::lang_feats_p19"])]
+    print(f"config3 lang_feats rel L2 ({mode}): {errs}")
+    assert max(errs) <= C3_BOUND[mode], (mode, errs)
+
+
 # ------------------------------------------------------------------------------------------
 # config-5 shape (ViT-L/14 patch 14 -> K 588 padded to 640, width 1024, 16 heads, T = 769,
 # RoBERTa-large width, N = 9 -> 72 pairs) with 2 + 2 layers

@@ -1,0 +1,72 @@
+#!/bin/bash
+# One GPU-box run recipe for every experiment (replaces the per-round rNN*.sh one-offs).
+# Run on the GPU box from the repo root:
+#   bash tools/gpu_run.sh TAG STEP [STEP ...]
+# Output goes to gpurun_out/TAG/. Each step has its own time limit. The first failing step ends
+# the script, and so does a time limit, an abort or a fault: nothing is retried.
+# Steps:
+#   tests[:ARGS]     pytest -m gpu over ARGS (default: tests)      -> pytest_gpu.log
+#   smoke            __graft_entry__.smoke()                          -> smoke.log
+#   bench[:ARGS]     python bench.py ARGS                             -> bench.log (appended)
+#   py:SCRIPT ARGS   python SCRIPT ARGS                               -> <script>.log (appended)
+#   attn-ab:NAME     rocprof kernel stats of tools/attn_bench.py, ab/libmmseq_NAME.so vs the
+#                    tree, alternated twice                           -> attn_{NAME,tree}_stats.csv
+#   epi-ab:NAME      tools/gemm_epi_bench.py, NAME vs tree, twice     -> epi_{NAME,tree}.log
+#   bench-ab:NAME    short bench (config 3 only), NAME vs tree, twice -> bench_{NAME,tree}.log
+#   kstats:SCRIPT ARGS  rocprof kernel stats of python SCRIPT ARGS    -> <script>_stats.csv
+#   profile          tools/profile_round.sh TAG (kernel stats + PMC of the default bench)
+set -euo pipefail
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+tag=${1:?tag}; shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+short="--no-cpu-baseline --no-config2 --no-config5 --no-rn50 --no-gemm-timer"
+
+with_lib() {  # with_lib NAME|tree -> sets MMSEQ_BENCH_LIB for the A/B variant
+  if [ "$1" = tree ]; then unset MMSEQ_BENCH_LIB; else export MMSEQ_BENCH_LIB=ab/libmmseq_$1.so; fi
+}
+
+kstats() {  # kstats DEST_CSV python-args...
+  local dest=$1; shift
+  local d="$out/kt_$$"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o kt -- \
+    python3 "$@" >> "${dest%.csv}.log" 2>&1
+  cat "$(find "$d" -name 'kt_kernel_stats.csv' | head -n1)" >> "$dest"
+  rm -rf "$d"
+}
+
+for step in "$@"; do
+  name=${step%%:*}; arg=""
+  [ "$name" != "$step" ] && arg=${step#*:}
+  echo "== $step" >&2
+  case $name in
+    tests)
+      timeout -k 10 900 python -u -m pytest -q -rs --maxfail 20 --timeout 300 --timeout-method thread \
+        ${arg:-tests} -m gpu > "$out/pytest_gpu.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 ;;
+    bench)
+      timeout -k 10 600 python -u bench.py $arg >> "$out/bench.log" 2>&1 ;;
+    py)
+      s=$(basename "${arg%% *}" .py)
+      timeout -k 10 600 python -u $arg >> "$out/$s.log" 2>&1 ;;
+    attn-ab|epi-ab|bench-ab)
+      for v in "$arg" tree "$arg" tree; do
+        with_lib "$v"
+        case $name in
+          attn-ab) kstats "$out/attn_${v}_stats.csv" tools/attn_bench.py 1 ;;
+          epi-ab) timeout -k 10 200 python3 tools/gemm_epi_bench.py 4 >> "$out/epi_$v.log" 2>&1 ;;
+          bench-ab) timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 $short --fwd-steps 0 \
+                      >> "$out/bench_$v.log" 2>&1 ;;
+        esac
+      done
+      unset MMSEQ_BENCH_LIB ;;
+    kstats)
+      s=$(basename "${arg%% *}" .py)
+      kstats "$out/${s}_stats.csv" $arg ;;
+    profile)
+      bash tools/profile_round.sh "$tag" ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
+echo "gpu_run $tag done" >&2
