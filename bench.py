@@ -275,23 +275,15 @@ def bench_config2(batch, steps, warmup, dev):
 def bench_config5(stories, micro, steps, warmup, dev):
     """BASELINE config 5 shape on one GPU (scripts/recipeqa_finetune.sh): ViT-L/14 (patch 14,
     1024 wide, 24 layers) + RoBERTa-large-shaped 24 x 1024 joint encoder, N = 9 steps -> 72 pairs
-    per story, 128 tokens per step -> T = 256 + 513 = 769, full training step in bf16, plus the
-    eval forward (no grad) in bf16 and with the MX-fp8 encoder GEMMs (kernels.fp8_forward,
-    v_mfma_scale_f32_16x16x128_f8f6f4): stories/s and the fp8 - bf16 loss difference."""
+    per story, 128 tokens per step -> T = 256 + 513 = 769: the full training step in bf16 and with
+    the fp8 forward GEMMs (kernels.fp8_forward(training=True): QKV / O / FC1 / FC2 of every ViT block
+    and joint layer on v_mfma_scale_f32_16x16x128_f8f6f4, backward bf16), plus the eval forward (no
+    grad) in bf16 and MX-fp8: stories/s, speedups and the fp8 - bf16 loss differences."""
     preset = model_zoo.PRESETS["config5"]
     m = model_zoo.build_preset("config5", device=dev, dtype=torch.bfloat16, seed=0)
-    m.train()
-    opt = FusedAdamW(m.stores(), lr=5e-6, warmup=100, total_steps=warmup + steps)
+    opt = FusedAdamW(m.stores(), lr=5e-6, warmup=100, total_steps=2 * (warmup + steps))
     data = synthetic_batch(stories, preset["N"], preset["per_seq"], 50265, 224, dev, seed=3000)
     mbs = [{k: v[o:o + micro] for k, v in data.items()} for o in range(0, stories, micro)]
-    for _ in range(warmup):
-        train_step(m, opt, mbs)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        loss = train_step(m, opt, mbs)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
     Nst, per = preset["N"], preset["per_seq"]
     V = m.bert.vision
     g = 224 // V["patch"]
@@ -299,7 +291,23 @@ def bench_config5(stories, micro, steps, warmup, dev):
     J = preset["joint"]
     fwd = story_flops(Nst * (Nst - 1), 2 * per, Tv, J["hidden_size"], J["num_hidden_layers"],
                       V["width"], V["layers"], V["patch"], V["embed"])
-    train_loss = float(loss.item())
+    train = {}
+    for name, fp8 in (("bf16", False), ("mxfp8_fwd", True)):
+        m.train()
+        with K.fp8_forward(fp8, training=True):
+            for _ in range(warmup):
+                train_step(m, opt, mbs)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                loss = train_step(m, opt, mbs)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        train[name] = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+                       "stories_per_s": stories * steps / dt,
+                       "model_tflops": stories * steps / dt * 3 * fwd / 1e12,
+                       "model_flops_util": stories * steps / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
+                       "loss": float(loss.item())}
     m.eval()
     fwd_legs = {}
     with torch.no_grad():
@@ -322,15 +330,17 @@ def bench_config5(stories, micro, steps, warmup, dev):
                                        max(1e-12, abs(fwd_legs["bf16"]["loss"])))
     del m, opt, mbs, data
     torch.cuda.empty_cache()
-    return {"workload": f"config5 shape: ViT-L/14 + 24x1024 joint encoder + BERSON, N={Nst}, "
-                        f"{Nst * (Nst - 1)} pairs/story, pair seq {2 * per}+{Tv}={2 * per + Tv}, "
-                        f"{stories} stories/step in micro-batches of {micro}, bf16, train mode, 1 GPU",
-            "steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
-            "stories_per_s": stories * steps / dt,
-            "model_tflops": stories * steps / dt * 3 * fwd / 1e12,
-            "model_flops_util": stories * steps / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
-            "fwd_tflop_per_story": fwd / 1e12, "loss": train_loss,
-            "eval_forward": fwd_legs}
+    out = {"workload": f"config5 shape: ViT-L/14 + 24x1024 joint encoder + BERSON, N={Nst}, "
+                       f"{Nst * (Nst - 1)} pairs/story, pair seq {2 * per}+{Tv}={2 * per + Tv}, "
+                       f"{stories} stories/step in micro-batches of {micro}, train mode (dropout), 1 GPU",
+           **train["bf16"], "fwd_tflop_per_story": fwd / 1e12,
+           "train_mxfp8_forward": dict(train["mxfp8_fwd"], speedup=train["mxfp8_fwd"]["steps_per_s"] /
+                                       train["bf16"]["steps_per_s"],
+                                       mode="kernels.fp8_forward(training=True): the four encoder "
+                                            "GEMMs of every layer's forward on the MX-fp8 MFMA, "
+                                            "backward bf16 (runs after the bf16 steps, same optimizer)"),
+           "eval_forward": fwd_legs}
+    return out
 
 
 def bench_config3_rn50(stories, micro, steps, warmup, dev):
@@ -607,7 +617,7 @@ def main():
             out["config3_rn50"] = {"error": repr(e)}
     if world == 1 and not args.no_config5:
         try:
-            out["config5"] = bench_config5(2, 1, 2, 1, dev)
+            out["config5"] = bench_config5(4, 2, 2, 1, dev)
         except Exception as e:
             out["config5"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

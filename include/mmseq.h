@@ -131,6 +131,16 @@ mmseq_status mmseq_attn_fwd_mxfp8(int P, int T, int heads, const void* qkv, int6
                                   int64_t q_off, int64_t k_off, int64_t v_off,
                                   const float* key_bias, float scale, float* lse, void* q8,
                                   int64_t ldq8, void* q8_scales, mmseq_stream stream);
+/* attn_fwd_mxfp8_dual: the same forward for a TRAINING step with the fp8 forward GEMMs (config 5):
+ *  the bf16 output O (for the backward; NULL: MX-fp8 only) and its MX-fp8 copy (the output
+ *  projection's operand) from one epilogue, with attention-probability dropout and keep bits as in
+ *  mmseq_attn_fwd (identical masks, O bit-identical to mmseq_attn_fwd variant 1). */
+mmseq_status mmseq_attn_fwd_mxfp8_dual(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                       int64_t q_off, int64_t k_off, int64_t v_off,
+                                       const float* key_bias, float scale, void* out,
+                                       int64_t ld_out, float* lse, const mmseq_dropout* drop,
+                                       uint64_t* keep_bits, void* q8, int64_t ldq8,
+                                       void* q8_scales, mmseq_stream stream);
 mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
                             int64_t q_off, int64_t k_off, int64_t v_off, const float* key_bias,
                             float scale, const void* out, int64_t ld_out, const void* dout,
@@ -412,6 +422,19 @@ mmseq_status mmseq_gemm_mxfp8_q8(int M, int N, int K, const void* A, int64_t lda
                                  const void* a_scales, const void* B, int64_t ldb,
                                  const void* b_scales, const float* bias, int act, void* q,
                                  int64_t ldq, void* q_scales, mmseq_stream stream);
+/* gemm_mxfp8_ex: the training-forward form (config 5 with the fp8 forward GEMMs; backward bf16):
+ *  C (bf16 [M][ldc]) = dropout(act(A B^T + bias)) + resid, aux (optional, needs act) = the bf16
+ *  pre-activation [M][ldc]; or, with q / q_scales, the MX-fp8 output quant(bf16(act(A B^T + bias)))
+ *  (no resid / drop) with C (optional) its bf16 copy and aux the pre-activation (FC1: what the
+ *  backward reads and FC2's fp8 operand, lxrt/modeling.py:467-493, clip/model.py:208-214).
+ *  The dropout mask is the bf16 GEMM's (mmseq_gemm) for the same descriptor. K % 256 == 0 and
+ *  M, N >= 256 (else MMSEQ_EUNSUPPORTED); ldc, ldr % 8, ldq % 16, 16-byte aligned buffers. */
+mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, int64_t lda,
+                                 const void* a_scales, const void* B, int64_t ldb,
+                                 const void* b_scales, void* C, int64_t ldc, const float* bias,
+                                 int act, void* aux, const void* resid, int64_t ldr,
+                                 const mmseq_dropout* drop, void* q, int64_t ldq, void* q_scales,
+                                 mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * CLIP ModifiedResNet / RN50 (clip/model.py:10-187; lxrt/modeling.py:621-705, 1014-1030), NHWC.

@@ -71,6 +71,10 @@ _SIGS = {
     "mmseq_attn_fwd_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _vp, _c_i64,
                                                            _vp, _vp]),
+    "mmseq_attn_fwd_mxfp8_dual": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64,
+                                                                      _c_i64, _vp, ctypes.c_float,
+                                                                      _vp, _c_i64, _vp, _dp, _vp,
+                                                                      _vp, _c_i64, _vp, _vp]),
     "mmseq_attn_keep_bits_words": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
@@ -138,6 +142,10 @@ _SIGS = {
                                                                 _vp]),
     "mmseq_gemm_mxfp8_q8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
                                                                _vp, ctypes.c_int, _vp, _c_i64, _vp,
+                                                               _vp]),
+    "mmseq_gemm_mxfp8_ex": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
+                                                               _vp, _c_i64, _vp, ctypes.c_int, _vp,
+                                                               _vp, _c_i64, _dp, _vp, _c_i64, _vp,
                                                                _vp]),
     "mmseq_conv_im2col": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_conv_col2im": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
@@ -548,6 +556,46 @@ def attn_fwd_mxfp8(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scal
                                       _p(key_bias), scale, _p(lse), _p(q), q.stride(0), _p(sc),
                                       _stream()), "mmseq_attn_fwd_mxfp8")
     return MXFP8(q, sc, rows_, cols)
+
+
+def attn_fwd_mxfp8_dual(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,
+                        lse, drop=None, keep_bits=None):
+    """Training attention forward with the bf16 output `out` (None: MX-fp8 only) AND its MX-fp8
+    copy (the fp8 output projection's operand), dropout / keep bits as attn_fwd
+    (mmseq_attn_fwd_mxfp8_dual) -> MXFP8 [P*T][heads*64]."""
+    rows_, cols = P * T, heads * 64
+    if out is not None:
+        _dev(out)
+    q = torch.empty(rows_, (cols + 15) // 16 * 16, dtype=torch.uint8, device=qkv.device)
+    sc = torch.zeros(lib().mmseq_mxfp8_scale_bytes(rows_, cols), dtype=torch.uint8, device=qkv.device)
+    _check(lib().mmseq_attn_fwd_mxfp8_dual(P, T, heads, _p(qkv), ld_qkv, q_off, k_off, v_off,
+                                           _p(key_bias), scale, _p(out), ld_out, _p(lse), _d(drop),
+                                           _p(keep_bits), _p(q), q.stride(0), _p(sc), _stream()),
+           "mmseq_attn_fwd_mxfp8_dual")
+    return MXFP8(q, sc, rows_, cols)
+
+
+def gemm_mxfp8_ex(a, b, c=None, bias=None, act=0, aux=None, resid=None, drop=None, q8=False):
+    """Training-forward fp8 GEMM (mmseq_gemm_mxfp8_ex): c (bf16) = dropout(act(a @ b^T + bias)) +
+    resid, aux = pre-activation; with q8=True also returns the MX-fp8 copy of the output (FC1: no
+    resid / drop). Returns the MXFP8 output (q8) or None."""
+    if a.K != b.K:
+        raise ValueError("gemm_mxfp8_ex: K mismatch")
+    rows, Nn = a.rows, b.rows
+    for t in (c, aux, resid):
+        if t is not None and (t.dtype != torch.bfloat16 or tuple(t.shape) != (rows, Nn)):
+            raise ValueError("gemm_mxfp8_ex: bf16 [rows][N] outputs / residual")
+    q = sc = None
+    if q8:
+        q = torch.empty(rows, (Nn + 15) // 16 * 16, dtype=torch.uint8, device=a.q.device)
+        sc = torch.empty(lib().mmseq_mxfp8_scale_bytes(rows, Nn), dtype=torch.uint8, device=a.q.device)
+    ld = c.stride(0) if c is not None else (aux.stride(0) if aux is not None else Nn)
+    _check(lib().mmseq_gemm_mxfp8_ex(rows, Nn, a.K, _p(a.q), a.q.stride(0), _p(a.scales), _p(b.q),
+                                     b.q.stride(0), _p(b.scales), _p(c), ld, _p(bias), act, _p(aux),
+                                     _p(resid), resid.stride(0) if resid is not None else 0, _d(drop),
+                                     _p(q), q.stride(0) if q is not None else 0, _p(sc), _stream()),
+           "mmseq_gemm_mxfp8_ex")
+    return MXFP8(q, sc, rows, Nn) if q8 else None
 
 
 def gemm_mxfp8(a, b, c, bias=None, act=0, resid=None, alpha=1.0):

@@ -914,6 +914,15 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
             pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
             *reinterpret_cast<int*>(a.q8 + row * a.ldq8 + h * 64 + (2 * b + dd) * 16 + 4 * g) = pk;
           }
+          if (a.o_w) {  // training: the bf16 output too (the backward's O), the same rounded values
+            unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + row * a.ld_out + h * 64 + 4 * g;
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd) {
+              typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+              *reinterpret_cast<u16x4*>(op + (2 * b + dd) * 16) =
+                  (u16x4){f2bf(v[4 * dd]), f2bf(v[4 * dd + 1]), f2bf(v[4 * dd + 2]), f2bf(v[4 * dd + 3])};
+            }
+          }
         }
       } else {
         unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
@@ -1903,27 +1912,50 @@ extern "C" int64_t mmseq_attn_keep_bits_words(int P, int T, int heads) {
   return (int64_t)P * heads * T * nkt2;
 }
 
-extern "C" mmseq_status mmseq_attn_fwd_mxfp8(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
-                                             int64_t q_off, int64_t k_off, int64_t v_off,
-                                             const float* key_bias, float scale, float* lse,
-                                             void* q8, int64_t ldq8, void* q8_scales,
-                                             mmseq_stream stream) {
+extern "C" mmseq_status mmseq_attn_fwd_mxfp8_dual(int P, int T, int heads, const void* qkv,
+                                                  int64_t ld_qkv, int64_t q_off, int64_t k_off,
+                                                  int64_t v_off, const float* key_bias, float scale,
+                                                  void* out, int64_t ld_out, float* lse,
+                                                  const mmseq_dropout* drop, uint64_t* keep_bits,
+                                                  void* q8, int64_t ldq8, void* q8_scales,
+                                                  mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, MMSEQ_BF16);
   if (st) return st;
   MMSEQ_REQUIRE(lse && q8 && q8_scales && ldq8 >= heads * 64 && ldq8 % 16 == 0 &&
                     ((uintptr_t)q8 & 15) == 0,
                 "attn_fwd_mxfp8: bad output (ldq8 % 16, 16-byte aligned)");
+  MMSEQ_REQUIRE(!out || (ld_out >= heads * 64 && ld_out % 4 == 0 && ((uintptr_t)out & 7) == 0),
+                "attn_fwd_mxfp8: bf16 out must be 8-byte aligned rows");
   if (P == 0) return MMSEQ_OK;
   AttnArgs a = {};
   a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
   a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
-  a.lse = lse; a.drop = make_drop(nullptr);
+  a.lse = lse; a.drop = make_drop(drop);
+  a.o_w = out; a.ld_out = ld_out;
   a.q8 = reinterpret_cast<uint8_t*>(q8); a.ldq8 = ldq8; a.q8s = reinterpret_cast<uint8_t*>(q8_scales);
   const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
   const int nkt = (T + 63) / 64;
   const size_t lds = (size_t)4 * 4096 * 2 + (size_t)nkt * (64 + 1) * 4;
   a.nkt2 = (nkt + 1) & ~1;
-  hipLaunchKernelGGL((attn_fwd_bf16_kernel<0, false, true>), gq, dim3(256), lds,
-                     reinterpret_cast<hipStream_t>(stream), a);
+  a.bits = keep_bits;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 1) & ~1)) / 2 + 64 >= (1ull << 32);
+  if (a.drop.thr && keep_bits)
+    hipLaunchKernelGGL((wide ? attn_fwd_bf16_kernel<2, true, true> : attn_fwd_bf16_kernel<2, false, true>),
+                       gq, dim3(256), lds, s, a);
+  else if (a.drop.thr)
+    hipLaunchKernelGGL((wide ? attn_fwd_bf16_kernel<1, true, true> : attn_fwd_bf16_kernel<1, false, true>),
+                       gq, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((attn_fwd_bf16_kernel<0, false, true>), gq, dim3(256), lds, s, a);
   return mmseq_check_launch("attn_fwd_mxfp8");
+}
+
+extern "C" mmseq_status mmseq_attn_fwd_mxfp8(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                             int64_t q_off, int64_t k_off, int64_t v_off,
+                                             const float* key_bias, float scale, float* lse,
+                                             void* q8, int64_t ldq8, void* q8_scales,
+                                             mmseq_stream stream) {
+  return mmseq_attn_fwd_mxfp8_dual(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale,
+                                   nullptr, 0, lse, nullptr, nullptr, q8, ldq8, q8_scales, stream);
 }

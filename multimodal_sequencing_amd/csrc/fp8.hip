@@ -382,6 +382,49 @@ extern "C" mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int
   return mmseq_check_launch("gemm_mxfp8");
 }
 
+// Training forward GEMM on the fp8 MFMA (BASELINE config 5): C (bf16) = dropout(act(A B^T + bias))
+// + resid with aux = the pre-activation, or, with q, the MX-fp8 output q + q_scales (and C then its
+// bf16 copy, aux the pre-activation; no residual / dropout): the MLP's FC1 writes what the backward
+// reads (bf16 GELU output and pre-activation) and FC2's fp8 operand in one epilogue. The 256 x 256
+// 8-phase F8 schedule only (K % 256 == 0, M and N >= 256); otherwise MMSEQ_EUNSUPPORTED.
+extern "C" mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, int64_t lda,
+                                            const void* a_scales, const void* B, int64_t ldb,
+                                            const void* b_scales, void* C, int64_t ldc,
+                                            const float* bias, int act, void* aux,
+                                            const void* resid, int64_t ldr,
+                                            const mmseq_dropout* drop, void* q, int64_t ldq,
+                                            void* q_scales, mmseq_stream stream) {
+  MMSEQ_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm_mxfp8_ex: sizes");
+  MMSEQ_REQUIRE(A && B && a_scales && b_scales && (C || q), "gemm_mxfp8_ex: null buffer");
+  MMSEQ_REQUIRE(!q == !q_scales, "gemm_mxfp8_ex: q and q_scales go together");
+  MMSEQ_REQUIRE(!aux || act, "gemm_mxfp8_ex: aux needs an activation");
+  MMSEQ_REQUIRE(act == 0 || act == MMSEQ_ACT_GELU_ERF || act == MMSEQ_ACT_QUICKGELU,
+                "gemm_mxfp8_ex: act");
+  if (M == 0) return MMSEQ_OK;
+  if (K % 256 != 0 || M < 256 || N < 256)
+    return mmseq_set_error(MMSEQ_EUNSUPPORTED, "gemm_mxfp8_ex: needs K %% 256 == 0 and M, N >= 256");
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K;
+  g.A = A; g.lda = lda; g.B = B; g.ldb = ldb;
+  g.bias = bias; g.act = act; g.aux = aux; g.resid = resid; g.ldr = resid ? ldr : 0;
+  g.alpha = 1.f; g.splitk = 1; g.kchunk = K;
+  g.drop = make_drop(drop);
+  if (q) {
+    g.C = q; g.ldc = ldq;
+    g.q8_scales = reinterpret_cast<uint8_t*>(q_scales);
+    g.cbf = C; g.ldcb = ldc;
+  } else {
+    g.C = C; g.ldc = ldc;
+  }
+  g.f8_sa = (const uint8_t*)a_scales; g.f8_sb = (const uint8_t*)b_scales;
+  g.f8_sa_bytes = mmseq_mxfp8_scale_bytes(M, K); g.f8_sb_bytes = mmseq_mxfp8_scale_bytes(N, K);
+  hipError_t e = hipSuccess;
+  MMSEQ_REQUIRE(mmseq_gemm256_nt_f8(g, mmseq_device_cus(), reinterpret_cast<hipStream_t>(stream), &e),
+                "gemm_mxfp8_ex: preconditions (leading dimensions, alignment, epilogue combination)");
+  if (e != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_mxfp8_ex launch: %s", hipGetErrorString(e));
+  return mmseq_check_launch("gemm_mxfp8_ex");
+}
+
 extern "C" mmseq_status mmseq_gemm_mxfp8_out(int M, int N, int K, const void* A, int64_t lda,
                                              const void* B, int64_t ldb, const float* bias,
                                              int act, void* q, int64_t ldq, void* scales,

@@ -727,7 +727,7 @@ extern "C" mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch, co
   float* const g_slab = reinterpret_cast<float*>(workspace);
   const int64_t g_slab_bytes = workspace ? workspace_bytes : 0;
   const int g_num_cu = sel.num_cu;
-  GemmArgs a;
+  GemmArgs a{};
   a.M = M; a.N = N; a.K = K;
   a.A = A; a.lda = lda; a.sA = strideA;
   a.B = B; a.ldb = ldb; a.sB = strideB;

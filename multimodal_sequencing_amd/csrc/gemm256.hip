@@ -141,6 +141,9 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
     v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
     v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
   }
+  const bool in = m < a.M && n < a.N;
+  const int64_t offb = (int64_t)m * a.ldcb + n;
+  if (ACT && a.aux && in) st8(reinterpret_cast<us*>(a.aux) + offb, v);  // training: pre-activation
   if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
@@ -154,6 +157,7 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
     v[r] = bf2f(f2bf(v[r]));
     amax = fmaxf(amax, fabsf(v[r]));
   }
+  if (a.cbf && in) st8(reinterpret_cast<us*>(a.cbf) + offb, v);  // training: the bf16 output too
   // max over lanes l ^ 16 and l ^ 32 with the gfx950 row swaps (no LDS round trip as with
   // ds_bpermute); amax >= 0, so its bit pattern orders like the value
   {
@@ -175,7 +179,7 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
     const uint32_t off = (uint32_t)(((m >> 6) * KB + (n >> 5)) * 64 + (m & 15) * 4 + ((m >> 4) & 3));
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(m < a.M ? e + 127 : 0), rq, off, 0, 0);
   }
-  if (m >= a.M || n >= a.N) return;
+  if (!in) return;
   uint32_t w[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -1060,10 +1064,15 @@ bool mmseq_gemm256_nt_f8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_
   auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   const bool q8 = a.q8_scales != nullptr;
   if (a.K % 256 != 0 || a.splitk != 1 || a.lda % 16 != 0 || a.ldb % 16 != 0 || !a16(a.A) ||
-      !a16(a.B) || !a.f8_sa || !a.f8_sb || a.aux || a.dact || a.accumulate || a.drop.thr || !a16(a.C))
+      !a16(a.B) || !a.f8_sa || !a.f8_sb || a.dact || a.accumulate || !a16(a.C))
     return false;
-  if (q8 ? (a.N % 32 != 0 || a.ldc % 16 != 0 || a.resid)
-         : (a.N % 8 != 0 || a.ldc % 8 != 0 || (a.resid && (a.ldr % 8 != 0 || !a16(a.resid)))))
+  if (a.aux && (!a16(a.aux) || !a.act)) return false;
+  // MX-fp8 out: no residual / dropout; its optional bf16 copy and aux share ldcb. bf16 out: the
+  // plain epilogue (bias, activation + aux, dropout, residual)
+  if (q8 ? (a.N % 32 != 0 || a.ldc % 16 != 0 || a.resid || a.drop.thr ||
+            ((a.cbf || a.aux) && (a.ldcb % 8 != 0 || (a.cbf && !a16(a.cbf)))))
+         : (a.N % 8 != 0 || a.ldc % 8 != 0 || a.cbf || (a.aux && a.ldc % 8 != 0) ||
+            (a.resid && (a.ldr % 8 != 0 || !a16(a.resid)))))
     return false;
   if (a.act != 0 && a.act != MMSEQ_ACT_GELU_ERF && a.act != MMSEQ_ACT_QUICKGELU) return false;
   const int tn = (a.N + 255) / 256;

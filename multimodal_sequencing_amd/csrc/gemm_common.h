@@ -19,6 +19,9 @@ struct GemmArgs {
   uint8_t* q8_scales;  // 256 NT kernel, MX-fp8 output: C is e4m3 [M][ldc] + these packed scales
   // 256 NT kernel, MX-fp8 operands (F8): A / B are e4m3 [rows][ld] with these packed E8M0 scales
   const uint8_t* f8_sa; const uint8_t* f8_sb; int64_t f8_sa_bytes, f8_sb_bytes;
+  // MX-fp8 output (q8_scales) of a training forward: the bf16 output too (cbf [M][ldcb]) and the
+  // pre-activation (aux, same layout) that the backward reads
+  void* cbf; int64_t ldcb;
 };
 
 template <typename TO>

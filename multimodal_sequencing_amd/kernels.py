@@ -50,23 +50,29 @@ def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=No
 # 256 8-phase schedule with MX-fp8 operands, gemm256.hip F8; weights quantised once per store
 # version, activations by mmseq_quant_mxfp8, FC1's output by its own epilogue for FC2). Shapes the
 # 8-phase form does not take (K or widths not multiples of 256) keep the round-2 path: FC1 bf16
-# with an MX-fp8 epilogue, FC2 fp8, QKV / O bf16. Training keeps bf16.
-_FP8 = {"on": False, "cache": {}}
+# with an MX-fp8 epilogue, FC2 fp8, QKV / O bf16. With training=True the TRAINING forward runs the
+# same four GEMMs on the fp8 MFMA too (the backward stays bf16): every producer writes the bf16
+# tensor the backward reads AND the next GEMM's MX-fp8 operand in one pass (LayerNorm, attention
+# mmseq_attn_fwd_mxfp8_dual, FC1 mmseq_gemm_mxfp8_ex with q), dropout masks as in bf16 training.
+_FP8 = {"on": False, "train": False, "cache": {}}
 
 
 class fp8_forward:
-    """Context manager: MX-fp8 encoder GEMMs in torch.no_grad() forwards."""
+    """Context manager: MX-fp8 encoder GEMMs in torch.no_grad() forwards (and, with
+    training=True, in the forward of training steps)."""
 
-    def __init__(self, enabled=True):
+    def __init__(self, enabled=True, training=False):
         self.enabled = enabled
+        self.training = training
 
     def __enter__(self):
-        self.prev = _FP8["on"]
+        self.prev = (_FP8["on"], _FP8["train"])
         _FP8["on"] = self.enabled
+        _FP8["train"] = self.enabled and self.training
         return self
 
     def __exit__(self, *exc):
-        _FP8["on"] = self.prev
+        _FP8["on"], _FP8["train"] = self.prev
         if not _FP8["on"]:
             _FP8["cache"].clear()
 
@@ -82,17 +88,27 @@ def _fp8_weight(st, W):
 
 def _f8(x, W):
     """The no-grad forward runs this GEMM on the fp8 MFMA: fp8_forward() on, bf16, K and the output
-    width multiples of 256 (the 256 x 256 8-phase kernel's MX-fp8 form)."""
+    width multiples of 256 (the 256 x 256 8-phase kernel's MX-fp8 form), and a hidden width the
+    fused MX-fp8 LayerNorm takes (<= 1024)."""
     K = x.shape[-1]
     return (_FP8["on"] and x.dtype == torch.bfloat16 and K % 256 == 0 and W.shape[0] % 256 == 0
-            and x.is_contiguous())
+            and K <= 1024 and x.is_contiguous())
+
+
+def _f8_train(x, *Ws):
+    """The training forward of a layer runs its GEMMs on the fp8 MFMA: fp8_forward(training=True),
+    every GEMM of the layer in the 8-phase MX-fp8 form (K and widths multiples of 256), >= 256 rows."""
+    return (_FP8["train"] and x.dtype == torch.bfloat16 and x.shape[0] >= 256 and x.shape[-1] <= 1024
+            and x.is_contiguous() and all(W.shape[0] % 256 == 0 and W.shape[1] % 256 == 0 for W in Ws))
 
 
 def _mx(x):
-    """The MX-fp8 copy of activation x: the one its producer (a fused LayerNorm) attached, else a
-    quantisation pass (mmseq_quant_mxfp8)."""
-    q = getattr(x, "_mx", None)
-    return q if q is not None else N.quant_mxfp8(x.view(-1, x.shape[-1]))
+    """The MX-fp8 copy of activation x: the one its producer (a fused LayerNorm) attached, if x has
+    not been modified since, else a quantisation pass (mmseq_quant_mxfp8)."""
+    hit = getattr(x, "_mx", None)
+    if hit is not None and hit[1] == x._version:
+        return hit[0]
+    return N.quant_mxfp8(x.view(-1, x.shape[-1]))
 
 
 def _lin8(st, x, W, bias=None, resid=None, xq=None):
@@ -110,7 +126,7 @@ def _ln8(x, gamma, beta, eps, y=None, mean=None, rstd=None):
     bf16 output too, its MX-fp8 copy attached for the next fp8 GEMM (_mx)."""
     q = N.layernorm_fwd_mxfp8(x.shape[0], x.shape[-1], x, gamma, beta, eps, y=y, mean=mean, rstd=rstd)
     if y is not None:
-        y._mx = q
+        y._mx = (q, y._version)  # valid while y is unmodified (_mx checks the version)
     return q
 
 
@@ -207,6 +223,8 @@ class BertLayerFn(torch.autograd.Function):
         d_att, d_o, d_out = drops
         Wqkv = st.packed(L.qkv_w, "w")
         bqkv = st.packed(L.qkv_b, "f32").view(-1)
+        if save and _f8_train(x, Wqkv, st.w(L.o_w), st.w(L.i_w), st.w(L.out_w)):
+            return BertLayerFn._forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv)
         f8 = not save and _f8(x, Wqkv) and d_att is None and d_o is None
         qkv = _lin8(st, x, Wqkv, bias=bqkv) if f8 else _linear(x, Wqkv, bias=bqkv)
         lse = torch.empty(P, heads, T, device=x.device)
@@ -249,6 +267,48 @@ class BertLayerFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    def _forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv):
+        """Training forward with QKV / O / FC1 / FC2 on the fp8 MFMA: the bf16 tensors the (bf16)
+        backward reads are written by the same producers that write the next GEMM's MX-fp8
+        operand (attention O, LayerNorm h1 / y, FC1's GELU output + pre-activation)."""
+        st = L.store
+        H = x.shape[-1]
+        R = x.shape[0]
+        d_att, d_o, d_out = drops
+        qkv = torch.empty(R, 3 * H, device=x.device, dtype=x.dtype)
+        N.gemm_mxfp8_ex(_mx(x), _fp8_weight(st, Wqkv), qkv, bias=bqkv)
+        lse = torch.empty(P, heads, T, device=x.device)
+        kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None else None
+        o = torch.empty_like(x)
+        oq = N.attn_fwd_mxfp8_dual(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias,
+                                   1.0 / math.sqrt(H // heads), o, H, lse, drop=d_att, keep_bits=kbits)
+        s1 = torch.empty_like(x)
+        N.gemm_mxfp8_ex(oq, _fp8_weight(st, st.w(L.o_w)), s1, bias=st.f32(L.o_b), resid=x, drop=d_o)
+        del oq
+        h1 = torch.empty_like(x)
+        m1 = torch.empty(R, device=x.device)
+        r1 = torch.empty_like(m1)
+        h1q = _ln8(s1, st.f32(L.ln1_w), st.f32(L.ln1_b), eps, mean=m1, rstd=r1, y=h1)
+        I = st.w(L.i_w).shape[0]
+        z = torch.empty(R, I, device=x.device, dtype=x.dtype)
+        gact = torch.empty_like(z)
+        gq = N.gemm_mxfp8_ex(h1q, _fp8_weight(st, st.w(L.i_w)), gact, bias=st.f32(L.i_b), act=GELU,
+                             aux=z, q8=True)
+        del h1q
+        s2 = torch.empty_like(x)
+        N.gemm_mxfp8_ex(gq, _fp8_weight(st, st.w(L.out_w)), s2, bias=st.f32(L.out_b), resid=h1,
+                        drop=d_out)
+        del gq
+        y = torch.empty_like(x)
+        m2 = torch.empty_like(m1)
+        r2 = torch.empty_like(m1)
+        _ln8(s2, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=y, mean=m2, rstd=r2)
+        ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
+        ctx.meta = (L, P, T, heads, drops)
+        ctx.kbits = kbits
+        return y
+
+    @staticmethod
     def _ffn_f8(st, L, x, s1, eps, d_out):
         """Eval fp8 tail of the layer: LN1 (bf16 out for the residual + MX-fp8 for FC1), FC1 ->
         FC2 on the fp8 MFMA, LN2 (bf16 out + MX-fp8 copy for the next layer's QKV)."""
@@ -260,6 +320,7 @@ class BertLayerFn(torch.autograd.Function):
             s2 = _mlp_fwd(st, h1, st.w(L.i_w), st.f32(L.i_b), GELU, st.w(L.out_w), st.f32(L.out_b),
                           h1, _linear, xq=h1q)
         else:
+            assert d_out is None, "eval fp8 path: the output dropout is off in inference"
             H = x.shape[-1]
             N.layernorm_fwd(s1.shape[0], H, s1, _rows(H), st.f32(L.ln1_w), st.f32(L.ln1_b), eps,
                             h1, _rows(H), m, r)
@@ -321,6 +382,8 @@ class VitBlockFn(torch.autograd.Function):
         R = h.shape[0]
         m1 = torch.empty(R, device=h.device)
         r1 = torch.empty_like(m1)
+        if save and _f8_train(h, st.w(L.in_w), st.w(L.out_w), st.w(L.fc_w), st.w(L.proj_w)):
+            return VitBlockFn._forward_f8_train(ctx, h, L, P, T, heads, eps, m1, r1)
         f8 = not save and _f8(h, st.w(L.in_w)) and _f8(h, st.w(L.fc_w))
         if f8:  # eval, fp8 GEMMs: the LayerNorm outputs are only GEMM operands -> MX-fp8 only
             hq = _ln8(h, st.f32(L.ln1_w), st.f32(L.ln1_b), eps, mean=m1, rstd=r1)
@@ -355,6 +418,42 @@ class VitBlockFn(torch.autograd.Function):
         z = torch.empty(R, st.w(L.fc_w).shape[0], device=h.device, dtype=h.dtype)
         gact = _linear(hn2, st.w(L.fc_w), bias=st.f32(L.fc_b), act=QGELU, aux=z)
         x2 = _linear(gact, st.w(L.proj_w), bias=st.f32(L.proj_b), resid=x1)
+        ctx.save_for_backward(h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact)
+        ctx.meta = (L, P, T, heads)
+        return x2
+
+    @staticmethod
+    def _forward_f8_train(ctx, h, L, P, T, heads, eps, m1, r1):
+        """Training forward with in_proj / out_proj / c_fc / c_proj on the fp8 MFMA (the LayerNorms
+        write the bf16 GEMM inputs the wgrads read plus the MX-fp8 operands; c_fc writes the
+        QuickGELU output, its pre-activation and c_proj's MX-fp8 operand)."""
+        st = L.store
+        W = h.shape[-1]
+        R = h.shape[0]
+        hn = torch.empty_like(h)
+        hq = _ln8(h, st.f32(L.ln1_w), st.f32(L.ln1_b), eps, y=hn, mean=m1, rstd=r1)
+        qkv = torch.empty(R, 3 * W, device=h.device, dtype=h.dtype)
+        N.gemm_mxfp8_ex(hq, _fp8_weight(st, st.w(L.in_w)), qkv, bias=st.f32(L.in_b))
+        del hq
+        lse = torch.empty(P, heads, T, device=h.device)
+        o = torch.empty_like(h)
+        oq = N.attn_fwd_mxfp8_dual(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None,
+                                   1.0 / math.sqrt(W // heads), o, W, lse)
+        x1 = torch.empty_like(h)
+        N.gemm_mxfp8_ex(oq, _fp8_weight(st, st.w(L.out_w)), x1, bias=st.f32(L.out_b), resid=h)
+        del oq
+        m2 = torch.empty_like(m1)
+        r2 = torch.empty_like(m1)
+        hn2 = torch.empty_like(h)
+        hq2 = _ln8(x1, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=hn2, mean=m2, rstd=r2)
+        F = st.w(L.fc_w).shape[0]
+        z = torch.empty(R, F, device=h.device, dtype=h.dtype)
+        gact = torch.empty_like(z)
+        gq = N.gemm_mxfp8_ex(hq2, _fp8_weight(st, st.w(L.fc_w)), gact, bias=st.f32(L.fc_b), act=QGELU,
+                             aux=z, q8=True)
+        del hq2
+        x2 = torch.empty_like(h)
+        N.gemm_mxfp8_ex(gq, _fp8_weight(st, st.w(L.proj_w)), x2, bias=st.f32(L.proj_b), resid=x1)
         ctx.save_for_backward(h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact)
         ctx.meta = (L, P, T, heads)
         return x2

@@ -232,3 +232,146 @@ def test_attention_mxfp8_out_matches_attention_then_quant(P, T, heads, masked):
     assert torch.equal(got.q[:, :H], want.q[:, :H])
     assert torch.equal(got.scales, want.scales)
     assert torch.equal(lse8, lse)
+
+
+# ---- the config-5 TRAINING forward on the fp8 MFMA (kernels.fp8_forward(training=True)) -------
+@pytest.mark.parametrize("P,T,heads,masked,mode", [(3, 513, 2, True, "bits"), (2, 393, 16, False, "none"),
+                                                   (1, 769, 4, True, "hash"), (2, 393, 2, False, "bits")])
+def test_attention_dual_out_matches_bf16_forward(P, T, heads, masked, mode):
+    """mmseq_attn_fwd_mxfp8_dual (training): its bf16 O is bit-identical to the bf16 forward's (same
+    dropout mask), its MX-fp8 O is that output quantised, and the keep bits / LSE are the same."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device="cpu").manual_seed(P * T + heads + 7)
+    H = heads * 64
+    qkv = torch.randn(P * T, 3 * H, generator=g).to(DEV, torch.bfloat16)
+    bias = None
+    if masked:
+        m = (torch.rand(P, T, generator=g) > 0.3).float()
+        m[:, 0] = 1
+        bias = ((1 - m) * -10000.0).to(DEV)
+    d = N.drop(0.1, 77, 1234) if mode != "none" else None
+    kb = N.attn_keep_bits(P, T, heads, DEV).zero_() if mode == "bits" else None
+    out = torch.empty(P * T, H, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(P, heads, T, device=DEV)
+    N.attn_set_fast(1)
+    N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, lse, drop=d, keep_bits=kb)
+    want = N.quant_mxfp8(out)
+    kb2 = N.attn_keep_bits(P, T, heads, DEV).zero_() if mode == "bits" else None
+    out2 = torch.full_like(out, 7.0)
+    lse2 = torch.empty_like(lse)
+    got = N.attn_fwd_mxfp8_dual(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out2, H, lse2,
+                                drop=d, keep_bits=kb2)
+    assert torch.equal(out2, out)
+    assert torch.equal(got.q[:, :H], want.q[:, :H])
+    assert torch.equal(got.scales, want.scales)
+    assert torch.equal(lse2, lse)
+    if kb is not None:
+        assert torch.equal(kb2, kb)
+
+
+@pytest.mark.parametrize("rows,Nn,K", [(600, 1024, 1024), (1000, 3072, 1024), (513, 1024, 4096)])
+def test_gemm_mxfp8_ex_epilogues(rows, Nn, K):
+    """mmseq_gemm_mxfp8_ex: (1) bias only == mmseq_gemm_mxfp8; (2) FC1 form (GELU, aux, MX-fp8 out +
+    its bf16 copy): aux == the pre-activation output, the bf16 copy == the GELU output, the MX-fp8 ==
+    that output quantised, all bit for bit; (3) O-proj / FC2 form (dropout + residual): the bf16 GEMM
+    epilogue's mask (mmseq_dropout_apply on the plain output) and the residual, to bf16 rounding."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows + Nn + K)
+    qa = N.quant_mxfp8(torch.randn(rows, K, device=DEV, generator=g).bfloat16())
+    qb = N.quant_mxfp8((torch.randn(Nn, K, device=DEV, generator=g) * 0.05).bfloat16())
+    b = torch.randn(Nn, device=DEV, generator=g) * 0.1
+    ref = torch.empty(rows, Nn, device=DEV, dtype=torch.bfloat16)
+    N.gemm_mxfp8(qa, qb, ref, bias=b)
+    y = torch.empty_like(ref)
+    N.gemm_mxfp8_ex(qa, qb, y, bias=b)
+    assert torch.equal(y, ref)
+    gelu = torch.empty_like(ref)
+    N.gemm_mxfp8(qa, qb, gelu, bias=b, act=1)
+    aux, gact = torch.empty_like(ref), torch.empty_like(ref)
+    q = N.gemm_mxfp8_ex(qa, qb, gact, bias=b, act=1, aux=aux, q8=True)
+    assert torch.equal(aux, ref) and torch.equal(gact, gelu)
+    want = N.quant_mxfp8(gelu)
+    assert torch.equal(q.q[:, :Nn], want.q[:, :Nn]) and torch.equal(q.scales, want.scales)
+    d = N.drop(0.1, 5, 99)
+    resid = torch.randn(rows, Nn, device=DEV, generator=g).bfloat16()
+    got = torch.empty_like(ref)
+    N.gemm_mxfp8_ex(qa, qb, got, bias=b, resid=resid, drop=d)
+    masked = torch.empty(rows, Nn, device=DEV)
+    N.dropout(ref.float(), masked, d)
+    exp = masked + resid.float()
+    keep = masked != 0
+    assert 0.87 < float(keep.float().mean()) < 0.93
+    torch.testing.assert_close(got.float(), exp, rtol=1e-2, atol=2e-2)
+    assert torch.equal(got.float()[~keep], resid.float()[~keep])  # dropped: exactly the residual
+
+
+def _c5_pair(steps_lr=1e-4):
+    import json
+    import os
+    from counter_init import counter_state_dict
+    from golden_util import GOLDEN
+    from make_golden_real import real_inputs
+    from multimodal_sequencing_amd import model_zoo
+    meta = json.load(open(os.path.join(GOLDEN, "real_config5_l2.json")))
+    models = []
+    for _ in range(2):
+        m = model_zoo.build_from_golden(meta["config"], device=DEV, dtype=torch.bfloat16)
+        sd = counter_state_dict({k: tuple(v.shape) for k, v in m.state_dict().items()})
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        models.append(m)
+    ids, labels, images = real_inputs(meta["input_seed"], meta["config"])
+    inputs = {"input_ids": torch.from_numpy(ids), "labels": torch.from_numpy(labels),
+              "images": torch.from_numpy(images).to(DEV)}
+    return meta, models, inputs
+
+
+def test_config5_fp8_training_forward_tracks_bf16():
+    """Config 5's fp8 training step (fp8_forward(training=True): QKV / O / FC1 / FC2 forward on the
+    fp8 MFMA, backward bf16) from the real_config5_l2 init: 3 AdamW steps (train mode, dropout on,
+    the same counter masks in both runs) track the bf16 run's losses within 1 %, the fp8 GEMMs really
+    run in the forward that autograd records, and the gradients point the same way."""
+    from multimodal_sequencing_amd import kernels as K
+    from multimodal_sequencing_amd.trainer import FusedAdamW, train_step
+    meta, (m16, m8), inputs = _c5_pair()
+    losses = {}
+    for name, m in (("bf16", m16), ("fp8", m8)):
+        m.train()
+        opt = FusedAdamW(m.stores(), lr=1e-5, warmup=0, total_steps=10)
+        with K.fp8_forward(name == "fp8", training=True):
+            ls = []
+            for _ in range(3):
+                ls.append(float(train_step(m, opt, [inputs])))
+            if name == "fp8":
+                assert len(K._FP8["cache"]) >= 16  # 4 weights x (2 ViT blocks + 2 joint layers)
+        losses[name] = ls
+    print(f"config5 3-step losses: bf16 {losses['bf16']}, fp8 forward {losses['fp8']}")
+    for a, b in zip(losses["fp8"], losses["bf16"]):
+        assert abs(a - b) < 1e-2 * abs(b), (losses)
+    assert losses["bf16"][-1] != losses["bf16"][0]  # the optimizer really moved the model
+
+
+def test_config5_fp8_training_forward_encoder_bound():
+    """The encoder output of the fp8 TRAINING forward (autograd recording, save=True path) against
+    the reference's lang_feats: within the MX-fp8 bound of the eval path (5e-2)."""
+    import numpy as np
+    from multimodal_sequencing_amd import kernels as K
+    from multimodal_sequencing_amd.process_inputs import prepare_berson_inputs
+    import os
+    from golden_util import GOLDEN
+    meta, (m, _), inputs = _c5_pair()
+    m.eval()
+    d = dict(np.load(os.path.join(GOLDEN, "real_config5_l2.npz")))
+    bi = prepare_berson_inputs(inputs["input_ids"], inputs["labels"], m.n_steps, device=DEV)
+    P, Lt = bi["input_ids"].shape[0] * bi["input_ids"].shape[1], bi["input_ids"].shape[2]
+    with K.fp8_forward(True, training=True):
+        joint, Lt = m.bert.encode_joint(bi["input_ids"].view(P, Lt), bi["attention_mask"].view(P, Lt),
+                                        bi["token_type_ids"].view(P, Lt), inputs["images"],
+                                        bi["pairs_list"])
+        assert joint.requires_grad and len(K._FP8["cache"]) >= 16
+    lang = joint[:, :Lt].detach().float().cpu().numpy()
+    errs = []
+    for got, key in ((lang[0], "i::lang_feats_p0"), (lang[-1], "i::lang_feats_p19")):
+        ref = d[key].astype(np.float64)
+        errs.append(float(np.linalg.norm(got - ref) / np.linalg.norm(ref)))
+    print(f"config5 fp8 training-forward lang_feats rel L2: {errs}")
+    assert max(errs) <= 5e-2, errs
