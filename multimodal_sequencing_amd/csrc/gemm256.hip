@@ -92,7 +92,11 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
     v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
     v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
   }
+#ifdef MMSEQ_EPI_SINK  // experiment: every tile stores into rows 0-255 (L2-resident, no HBM writes)
+  const int64_t off = (int64_t)(m & 255) * a.ldc + n;
+#else
   const int64_t off = (int64_t)m * a.ldc + n;
+#endif
   if (BWD) {
     if (DTAB) {
 #pragma unroll
