@@ -281,7 +281,7 @@ def bench_config5(stories, micro, steps, warmup, dev):
     grad) in bf16 and MX-fp8: stories/s, speedups and the fp8 - bf16 loss differences."""
     preset = model_zoo.PRESETS["config5"]
     m = model_zoo.build_preset("config5", device=dev, dtype=torch.bfloat16, seed=0)
-    opt = FusedAdamW(m.stores(), lr=5e-6, warmup=100, total_steps=2 * (warmup + steps))
+    opt = FusedAdamW(m.stores(), lr=5e-6, warmup=100, total_steps=3 * (warmup + steps))
     data = synthetic_batch(stories, preset["N"], preset["per_seq"], 50265, 224, dev, seed=3000)
     mbs = [{k: v[o:o + micro] for k, v in data.items()} for o in range(0, stories, micro)]
     Nst, per = preset["N"], preset["per_seq"]
@@ -292,9 +292,10 @@ def bench_config5(stories, micro, steps, warmup, dev):
     fwd = story_flops(Nst * (Nst - 1), 2 * per, Tv, J["hidden_size"], J["num_hidden_layers"],
                       V["width"], V["layers"], V["patch"], V["embed"])
     train = {}
-    for name, fp8 in (("bf16", False), ("mxfp8_fwd", True)):
+    for name, fp8, dg in (("bf16", False, False), ("mxfp8_fwd", True, False),
+                          ("mxfp8_fwd_dgrad", True, True)):
         m.train()
-        with K.fp8_forward(fp8, training=True):
+        with K.fp8_forward(fp8, training=True, dgrad=dg):
             for _ in range(warmup):
                 train_step(m, opt, mbs)
             torch.cuda.synchronize()
@@ -339,6 +340,13 @@ def bench_config5(stories, micro, steps, warmup, dev):
                                        mode="kernels.fp8_forward(training=True): the four encoder "
                                             "GEMMs of every layer's forward on the MX-fp8 MFMA, "
                                             "backward bf16 (runs after the bf16 steps, same optimizer)"),
+           "train_mxfp8_forward_dgrad": dict(train["mxfp8_fwd_dgrad"],
+                                             speedup=train["mxfp8_fwd_dgrad"]["steps_per_s"] /
+                                             train["bf16"]["steps_per_s"],
+                                             mode="fp8_forward(training=True, dgrad=True): also the "
+                                                  "four data-gradient GEMMs of every layer on the "
+                                                  "MX-fp8 MFMA (dY quantised per call); weight "
+                                                  "gradients bf16"),
            "eval_forward": fwd_legs}
     return out
 

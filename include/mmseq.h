@@ -427,12 +427,14 @@ mmseq_status mmseq_gemm_mxfp8_q8(int M, int N, int K, const void* A, int64_t lda
  *  pre-activation [M][ldc]; or, with q / q_scales, the MX-fp8 output quant(bf16(act(A B^T + bias)))
  *  (no resid / drop) with C (optional) its bf16 copy and aux the pre-activation (FC1: what the
  *  backward reads and FC2's fp8 operand, lxrt/modeling.py:467-493, clip/model.py:208-214).
- *  The dropout mask is the bf16 GEMM's (mmseq_gemm) for the same descriptor. K % 256 == 0 and
+ *  With dact (and act, nothing else): the dgrad form C = (A B^T) * act'(dact), dact bf16 [M][ldc]
+ *  (the backward's fp8 dgrad: dz = dY W * GELU'(z)). The dropout mask is the bf16 GEMM's
+ *  (mmseq_gemm) for the same descriptor. K % 256 == 0 and
  *  M, N >= 256 (else MMSEQ_EUNSUPPORTED); ldc, ldr % 8, ldq % 16, 16-byte aligned buffers. */
 mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, int64_t lda,
                                  const void* a_scales, const void* B, int64_t ldb,
                                  const void* b_scales, void* C, int64_t ldc, const float* bias,
-                                 int act, void* aux, const void* resid, int64_t ldr,
+                                 int act, void* aux, const void* dact, const void* resid, int64_t ldr,
                                  const mmseq_dropout* drop, void* q, int64_t ldq, void* q_scales,
                                  mmseq_stream stream);
 

@@ -145,8 +145,8 @@ _SIGS = {
                                                                _vp]),
     "mmseq_gemm_mxfp8_ex": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _c_i64, _vp,
                                                                _vp, _c_i64, _vp, ctypes.c_int, _vp,
-                                                               _vp, _c_i64, _dp, _vp, _c_i64, _vp,
-                                                               _vp]),
+                                                               _vp, _vp, _c_i64, _dp, _vp, _c_i64,
+                                                               _vp, _vp]),
     "mmseq_conv_im2col": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_conv_col2im": (ctypes.c_int, [ctypes.c_int] * 8 + [_vp, _vp, ctypes.c_int, _vp]),
     "mmseq_bn_workspace": (ctypes.c_int64, [_c_i64, ctypes.c_int]),
@@ -575,14 +575,16 @@ def attn_fwd_mxfp8_dual(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias,
     return MXFP8(q, sc, rows_, cols)
 
 
-def gemm_mxfp8_ex(a, b, c=None, bias=None, act=0, aux=None, resid=None, drop=None, q8=False):
-    """Training-forward fp8 GEMM (mmseq_gemm_mxfp8_ex): c (bf16) = dropout(act(a @ b^T + bias)) +
-    resid, aux = pre-activation; with q8=True also returns the MX-fp8 copy of the output (FC1: no
-    resid / drop). Returns the MXFP8 output (q8) or None."""
+def gemm_mxfp8_ex(a, b, c=None, bias=None, act=0, aux=None, resid=None, drop=None, q8=False,
+                  dact=None):
+    """Training fp8 GEMM (mmseq_gemm_mxfp8_ex): c (bf16) = dropout(act(a @ b^T + bias)) + resid,
+    aux = pre-activation; with q8=True also returns the MX-fp8 copy of the output (FC1: no resid /
+    drop); with dact the dgrad form c = (a @ b^T) * act'(dact). Returns the MXFP8 output (q8) or
+    None."""
     if a.K != b.K:
         raise ValueError("gemm_mxfp8_ex: K mismatch")
     rows, Nn = a.rows, b.rows
-    for t in (c, aux, resid):
+    for t in (c, aux, resid, dact):
         if t is not None and (t.dtype != torch.bfloat16 or tuple(t.shape) != (rows, Nn)):
             raise ValueError("gemm_mxfp8_ex: bf16 [rows][N] outputs / residual")
     q = sc = None
@@ -592,7 +594,7 @@ def gemm_mxfp8_ex(a, b, c=None, bias=None, act=0, aux=None, resid=None, drop=Non
     ld = c.stride(0) if c is not None else (aux.stride(0) if aux is not None else Nn)
     _check(lib().mmseq_gemm_mxfp8_ex(rows, Nn, a.K, _p(a.q), a.q.stride(0), _p(a.scales), _p(b.q),
                                      b.q.stride(0), _p(b.scales), _p(c), ld, _p(bias), act, _p(aux),
-                                     _p(resid), resid.stride(0) if resid is not None else 0, _d(drop),
+                                     _p(dact), _p(resid), resid.stride(0) if resid is not None else 0, _d(drop),
                                      _p(q), q.stride(0) if q is not None else 0, _p(sc), _stream()),
            "mmseq_gemm_mxfp8_ex")
     return MXFP8(q, sc, rows, Nn) if q8 else None

@@ -382,22 +382,25 @@ extern "C" mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int
   return mmseq_check_launch("gemm_mxfp8");
 }
 
-// Training forward GEMM on the fp8 MFMA (BASELINE config 5): C (bf16) = dropout(act(A B^T + bias))
-// + resid with aux = the pre-activation, or, with q, the MX-fp8 output q + q_scales (and C then its
-// bf16 copy, aux the pre-activation; no residual / dropout): the MLP's FC1 writes what the backward
-// reads (bf16 GELU output and pre-activation) and FC2's fp8 operand in one epilogue. The 256 x 256
-// 8-phase F8 schedule only (K % 256 == 0, M and N >= 256); otherwise MMSEQ_EUNSUPPORTED.
+// Training GEMM on the fp8 MFMA (BASELINE config 5): C (bf16) = dropout(act(A B^T + bias)) + resid
+// with aux = the pre-activation, or, with q, the MX-fp8 output q + q_scales (and C then its bf16
+// copy, aux the pre-activation; no residual / dropout): the MLP's FC1 writes what the backward reads
+// (bf16 GELU output and pre-activation) and FC2's fp8 operand in one epilogue; or, with dact, the
+// dgrad form C = (A B^T) * act'(dact). The 256 x 256 8-phase F8 schedule only (K % 256 == 0, M and
+// N >= 256); otherwise MMSEQ_EUNSUPPORTED.
 extern "C" mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, int64_t lda,
                                             const void* a_scales, const void* B, int64_t ldb,
                                             const void* b_scales, void* C, int64_t ldc,
                                             const float* bias, int act, void* aux,
-                                            const void* resid, int64_t ldr,
+                                            const void* dact, const void* resid, int64_t ldr,
                                             const mmseq_dropout* drop, void* q, int64_t ldq,
                                             void* q_scales, mmseq_stream stream) {
   MMSEQ_REQUIRE(M >= 0 && N > 0 && K > 0, "gemm_mxfp8_ex: sizes");
   MMSEQ_REQUIRE(A && B && a_scales && b_scales && (C || q), "gemm_mxfp8_ex: null buffer");
   MMSEQ_REQUIRE(!q == !q_scales, "gemm_mxfp8_ex: q and q_scales go together");
   MMSEQ_REQUIRE(!aux || act, "gemm_mxfp8_ex: aux needs an activation");
+  MMSEQ_REQUIRE(!dact || (act && !aux && !resid && !bias && !q && !(drop && drop->p > 0.f)),
+                "gemm_mxfp8_ex: dact (dgrad) takes an activation and nothing else");
   MMSEQ_REQUIRE(act == 0 || act == MMSEQ_ACT_GELU_ERF || act == MMSEQ_ACT_QUICKGELU,
                 "gemm_mxfp8_ex: act");
   if (M == 0) return MMSEQ_OK;
@@ -406,7 +409,7 @@ extern "C" mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, 
   GemmArgs g{};
   g.M = M; g.N = N; g.K = K;
   g.A = A; g.lda = lda; g.B = B; g.ldb = ldb;
-  g.bias = bias; g.act = act; g.aux = aux; g.resid = resid; g.ldr = resid ? ldr : 0;
+  g.bias = bias; g.act = act; g.aux = aux; g.dact = dact; g.resid = resid; g.ldr = resid ? ldr : 0;
   g.alpha = 1.f; g.splitk = 1; g.kchunk = K;
   g.drop = make_drop(drop);
   if (q) {

@@ -68,6 +68,11 @@ __device__ __forceinline__ EpiBias epi_bias(const GemmArgs& a, int n) {
 // 2 signs = 3328 fp32 entries, 13 KB of LDS), exact (libm erf / exp at kernel start). |z| outside
 // clamps to the range ends, where act' is within 8e-4 of its limit (0.5 near 0; 0 or 1 beyond 8).
 // One LDS gather per element instead of ~17 VALU slots of a fitted GELU' (two transcendentals).
+// The table holds the EXACT derivative on purpose: the reference's backward is the exact GELU' (its
+// forward the exact erf GELU), so the dgrad evaluates the reference's derivative at our stored
+// pre-activation; the forward epilogue's fitted logistic (gelu_sig, 2.5e-5 abs) differs from it by
+// <= 1.1e-4, far below the bf16 quantum. gelu_sig_grad (the fit's own derivative) is only used by
+// the non-default two-block variant (gemm_nt_2b_kernel).
 constexpr int DT_LO = 117 << 7;  // bf16 bits of 2^-10
 constexpr int DT_N = 13 * 128;   // entries per sign
 __device__ __forceinline__ int dtab_index(unsigned short u) {
@@ -289,7 +294,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
   // the 2 x 2 KB scale buffers
   __shared__ __attribute__((aligned(16))) unsigned short
       smem[2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0) + (F8 ? 2048 : 0) + 1024];
-  unsigned short* const sscale = smem + 2 * 2 * G_LDA_HALF;  // F8: [2 buffers][A 1 KB | B 1 KB]
+  // F8: [2 buffers][A 1 KB | B 1 KB], after the dgrad variants' activation-derivative table
+  unsigned short* const sscale = smem + 2 * 2 * G_LDA_HALF + (BWD ? 4 * DT_N : 0);
   // the tile's 256 bias values, [2 tiles][1 KB]: DMA'd by wave 0 before the tile's K-loop (older
   // than the first iteration's stages, so retired by its phase-4 counted wait and visible after
   // that phase's barrier), read by the epilogue from LDS. A global bias load in the epilogue was
@@ -1068,9 +1074,11 @@ bool mmseq_gemm256_nt_f8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_
   auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   const bool q8 = a.q8_scales != nullptr;
   if (a.K % 256 != 0 || a.splitk != 1 || a.lda % 16 != 0 || a.ldb % 16 != 0 || !a16(a.A) ||
-      !a16(a.B) || !a.f8_sa || !a.f8_sb || a.dact || a.accumulate || !a16(a.C))
+      !a16(a.B) || !a.f8_sa || !a.f8_sb || a.accumulate || !a16(a.C))
     return false;
   if (a.aux && (!a16(a.aux) || !a.act)) return false;
+  // dgrad form: C = (A B^T) * act'(dact) (the activation derivative at the stored pre-activation)
+  if (a.dact && (!a.act || q8 || a.resid || a.aux || a.bias || a.drop.thr || !a16(a.dact))) return false;
   // MX-fp8 out: no residual / dropout; its optional bf16 copy and aux share ldcb. bf16 out: the
   // plain epilogue (bias, activation + aux, dropout, residual)
   if (q8 ? (a.N % 32 != 0 || a.ldc % 16 != 0 || a.resid || a.drop.thr ||
@@ -1084,7 +1092,12 @@ bool mmseq_gemm256_nt_f8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_
   const dim3 grid(ntiles < num_cu ? ntiles : num_cu), block(512);
 #define F8_LAUNCH(ACT, XIN, Q8) \
   hipLaunchKernelGGL((gemm256_nt_kernel<ACT, false, XIN, Q8, true>), grid, block, 0, s, a, tn, ntiles, 0)
-  if (q8) {
+  if (a.dact) {
+    if (a.act == MMSEQ_ACT_GELU_ERF)
+      hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, true, true, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
+    else
+      hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, true, true, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
+  } else if (q8) {
     if (a.act == MMSEQ_ACT_GELU_ERF) F8_LAUNCH(MMSEQ_ACT_GELU_ERF, false, true);
     else if (a.act == MMSEQ_ACT_QUICKGELU) F8_LAUNCH(MMSEQ_ACT_QUICKGELU, false, true);
     else F8_LAUNCH(0, false, true);

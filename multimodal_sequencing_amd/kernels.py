@@ -54,25 +54,28 @@ def _linear(x, W, bias=None, act=0, aux=None, resid=None, out=None, out_dtype=No
 # same four GEMMs on the fp8 MFMA too (the backward stays bf16): every producer writes the bf16
 # tensor the backward reads AND the next GEMM's MX-fp8 operand in one pass (LayerNorm, attention
 # mmseq_attn_fwd_mxfp8_dual, FC1 mmseq_gemm_mxfp8_ex with q), dropout masks as in bf16 training.
-_FP8 = {"on": False, "train": False, "cache": {}}
+_FP8 = {"on": False, "train": False, "dgrad": False, "cache": {}}
 
 
 class fp8_forward:
     """Context manager: MX-fp8 encoder GEMMs in torch.no_grad() forwards (and, with
-    training=True, in the forward of training steps)."""
+    training=True, in the forward of training steps; with dgrad=True also the backward's four
+    data-gradient GEMMs of those layers, dY quantised per call; weight gradients stay bf16)."""
 
-    def __init__(self, enabled=True, training=False):
+    def __init__(self, enabled=True, training=False, dgrad=False):
         self.enabled = enabled
         self.training = training
+        self.dgrad = dgrad
 
     def __enter__(self):
-        self.prev = (_FP8["on"], _FP8["train"])
+        self.prev = (_FP8["on"], _FP8["train"], _FP8["dgrad"])
         _FP8["on"] = self.enabled
         _FP8["train"] = self.enabled and self.training
+        _FP8["dgrad"] = self.enabled and self.training and self.dgrad
         return self
 
     def __exit__(self, *exc):
-        _FP8["on"], _FP8["train"] = self.prev
+        _FP8["on"], _FP8["train"], _FP8["dgrad"] = self.prev
         if not _FP8["on"]:
             _FP8["cache"].clear()
 
@@ -152,6 +155,16 @@ def _mlp_fwd(st, x, Wi, bi, act, Wo, bo, resid, lin, xq=None):
         N.gemm_mxfp8(q, _fp8_weight(st, Wo), out, bias=bo, resid=resid.view(R, -1))
         return out
     return lin(lin(x, Wi, bias=bi, act=act), Wo, bias=bo, resid=resid)
+
+
+def _dgrad8(dy, st, WT, resid=None, act=0, dact=None):
+    """dx = dy W (+ resid) or (dy W) * act'(dact) on the fp8 MFMA: dy quantised to MX-fp8 here,
+    the transposed weight shadow WT [in][out] once per store version (config 5, dgrad=True)."""
+    R = dy.numel() // dy.shape[-1]
+    out = torch.empty(R, WT.shape[0], device=dy.device, dtype=dy.dtype)
+    N.gemm_mxfp8_ex(N.quant_mxfp8(dy.view(R, -1)), _fp8_weight(st, WT), out, act=act, dact=dact,
+                    resid=resid)
+    return out
 
 
 def _dgrad(dy, WT, resid=None, act=0, dact=None, out=None):
@@ -306,6 +319,7 @@ class BertLayerFn(torch.autograd.Function):
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
         ctx.meta = (L, P, T, heads, drops)
         ctx.kbits = kbits
+        ctx.f8dg = _FP8["dgrad"]
         return y
 
     @staticmethod
@@ -346,11 +360,13 @@ class BertLayerFn(torch.autograd.Function):
         N.layernorm_bwd(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
                         None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b),
                         dx_drop=ds2d if d_out is not None else None, drop_dx=d_out)
+        f8 = getattr(ctx, "f8dg", False)
+        dg = (lambda d, WT, **kw: _dgrad8(d, st, WT, **kw)) if f8 else _dgrad
         _wgrad(ds2d, gact, st.g(L.out_w), st.g(L.out_b))
-        dz = _dgrad(ds2d, st.wt(L.out_w), act=GELU, dact=z)
+        dz = dg(ds2d, st.wt(L.out_w), act=GELU, dact=z)
         del ds2d
         _wgrad(dz, h1, st.g(L.i_w), st.g(L.i_b))
-        dh1 = _dgrad(dz, st.wt(L.i_w), resid=ds2)
+        dh1 = dg(dz, st.wt(L.i_w), resid=ds2)
         del dz
         ds1 = torch.empty_like(dy)
         ds1d = torch.empty_like(dy) if d_o is not None else ds1
@@ -358,7 +374,7 @@ class BertLayerFn(torch.autograd.Function):
                         None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
                         dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
         _wgrad(ds1d, o, st.g(L.o_w), st.g(L.o_b))
-        do = _dgrad(ds1d, st.wt(L.o_w))
+        do = dg(ds1d, st.wt(L.o_w))
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
@@ -367,7 +383,7 @@ class BertLayerFn(torch.autograd.Function):
         ctx.kbits = None
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         st.grad_ready(L.span)
-        dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
+        dx = dg(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None, None
 
 
@@ -456,6 +472,7 @@ class VitBlockFn(torch.autograd.Function):
         N.gemm_mxfp8_ex(gq, _fp8_weight(st, st.w(L.proj_w)), x2, bias=st.f32(L.proj_b), resid=x1)
         ctx.save_for_backward(h, m1, r1, hn, qkv, o, lse, x1, m2, r2, hn2, z, gact)
         ctx.meta = (L, P, T, heads)
+        ctx.f8dg = _FP8["dgrad"]
         return x2
 
     @staticmethod
@@ -467,22 +484,24 @@ class VitBlockFn(torch.autograd.Function):
         W = h.shape[-1]
         R = h.shape[0]
         dx2 = dx2.contiguous()
+        f8 = getattr(ctx, "f8dg", False)
+        dg = (lambda d, WT, **kw: _dgrad8(d, st, WT, **kw)) if f8 else _dgrad
         _wgrad(dx2, gact, st.g(L.proj_w), st.g(L.proj_b))
-        dz = _dgrad(dx2, st.wt(L.proj_w), act=QGELU, dact=z)
+        dz = dg(dx2, st.wt(L.proj_w), act=QGELU, dact=z)
         _wgrad(dz, hn2, st.g(L.fc_w), st.g(L.fc_b))
-        dhn2 = _dgrad(dz, st.wt(L.fc_w))
+        dhn2 = dg(dz, st.wt(L.fc_w))
         del dz
         dx1 = torch.empty_like(h)
         N.layernorm_bwd(R, W, dhn2, _rows(W), x1, _rows(W), m2, r2, st.f32(L.ln2_w), dx1, _rows(W),
                         dx2, _rows(W), st.g(L.ln2_w), st.g(L.ln2_b))
         _wgrad(dx1, o, st.g(L.out_w), st.g(L.out_b))
-        do = _dgrad(dx1, st.wt(L.out_w))
+        do = dg(dx1, st.wt(L.out_w))
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=h.device)
         N.attn_bwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
                    do, W, lse, delta, dqkv, 3 * W)
         _wgrad(dqkv, hn, st.g(L.in_w), st.g(L.in_b))
-        dhn = _dgrad(dqkv, st.wt(L.in_w))
+        dhn = dg(dqkv, st.wt(L.in_w))
         dh = torch.empty_like(h)
         N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
                         dx1, _rows(W), st.g(L.ln1_w), st.g(L.ln1_b))

@@ -305,6 +305,29 @@ def test_gemm_mxfp8_ex_epilogues(rows, Nn, K):
     assert torch.equal(got.float()[~keep], resid.float()[~keep])  # dropped: exactly the residual
 
 
+@pytest.mark.parametrize("rows,Nn,K,act", [(600, 4096, 1024, 1), (513, 1024, 4096, 2)])
+def test_gemm_mxfp8_ex_dgrad_epilogue(rows, Nn, K, act):
+    """The fp8 dgrad form (mmseq_gemm_mxfp8_ex with dact): (A B^T) * act'(dact) against the same fp8
+    product's bf16 output times the exact derivative (torch), to bf16 rounding."""
+    import math
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows + Nn + K + act)
+    qa = N.quant_mxfp8(torch.randn(rows, K, device=DEV, generator=g).bfloat16())
+    qb = N.quant_mxfp8((torch.randn(Nn, K, device=DEV, generator=g) * 0.05).bfloat16())
+    z = (torch.randn(rows, Nn, device=DEV, generator=g) * 2).bfloat16()
+    plain = torch.empty(rows, Nn, device=DEV, dtype=torch.bfloat16)
+    N.gemm_mxfp8(qa, qb, plain)
+    got = torch.empty_like(plain)
+    N.gemm_mxfp8_ex(qa, qb, got, act=act, dact=z)
+    zf = z.float()
+    if act == 1:
+        d = 0.5 * (1 + torch.erf(zf / math.sqrt(2))) + zf * torch.exp(-0.5 * zf * zf) / math.sqrt(2 * math.pi)
+    else:
+        sg = torch.sigmoid(1.702 * zf)
+        d = sg + 1.702 * zf * sg * (1 - sg)
+    torch.testing.assert_close(got.float(), plain.float() * d, rtol=2e-2, atol=2e-2)
+
+
 def _c5_pair(steps_lr=1e-4):
     import json
     import os
@@ -327,26 +350,38 @@ def _c5_pair(steps_lr=1e-4):
 
 def test_config5_fp8_training_forward_tracks_bf16():
     """Config 5's fp8 training step (fp8_forward(training=True): QKV / O / FC1 / FC2 forward on the
-    fp8 MFMA, backward bf16) from the real_config5_l2 init: 3 AdamW steps (train mode, dropout on,
-    the same counter masks in both runs) track the bf16 run's losses within 1 %, the fp8 GEMMs really
-    run in the forward that autograd records, and the gradients point the same way."""
+    fp8 MFMA, backward bf16; and with dgrad=True the four data-gradient GEMMs too) from the
+    real_config5_l2 init: 3 AdamW steps (train mode, dropout on, the same counter masks in every run)
+    track the bf16 run's losses within 1 %, the fp8 GEMMs really run, and the first step's full
+    gradient points the same way as bf16's (cosine > 0.99)."""
     from multimodal_sequencing_amd import kernels as K
     from multimodal_sequencing_amd.trainer import FusedAdamW, train_step
     meta, (m16, m8), inputs = _c5_pair()
-    losses = {}
-    for name, m in (("bf16", m16), ("fp8", m8)):
+    m8d = _c5_pair()[1][0]
+    losses, grads = {}, {}
+    for name, m in (("bf16", m16), ("fp8", m8), ("fp8_dgrad", m8d)):
         m.train()
         opt = FusedAdamW(m.stores(), lr=1e-5, warmup=0, total_steps=10)
-        with K.fp8_forward(name == "fp8", training=True):
+        with K.fp8_forward(name != "bf16", training=True, dgrad=name == "fp8_dgrad"):
             ls = []
-            for _ in range(3):
+            for i in range(3):
+                if i == 0:  # the first step's gradients, before the update
+                    m.zero_grad()
+                    m(inputs)[0].backward()
+                    grads[name] = torch.cat([s.grad.clone() for s in m.stores()])
+                    m.zero_grad()
                 ls.append(float(train_step(m, opt, [inputs])))
-            if name == "fp8":
-                assert len(K._FP8["cache"]) >= 16  # 4 weights x (2 ViT blocks + 2 joint layers)
+            if name != "bf16":
+                assert len(K._FP8["cache"]) >= (32 if name == "fp8_dgrad" else 16)
         losses[name] = ls
-    print(f"config5 3-step losses: bf16 {losses['bf16']}, fp8 forward {losses['fp8']}")
-    for a, b in zip(losses["fp8"], losses["bf16"]):
-        assert abs(a - b) < 1e-2 * abs(b), (losses)
+    print(f"config5 3-step losses: {losses}")
+    for name in ("fp8", "fp8_dgrad"):
+        for a, b in zip(losses[name], losses["bf16"]):
+            assert abs(a - b) < 1e-2 * abs(b), (name, losses)
+        g, r = grads[name].double(), grads["bf16"].double()
+        cos = float(g @ r / (g.norm() * r.norm()))
+        print(f"{name}: first-step gradient cosine vs bf16 {cos:.5f}, norm ratio {float(g.norm() / r.norm()):.4f}")
+        assert cos > 0.99, (name, cos)
     assert losses["bf16"][-1] != losses["bf16"][0]  # the optimizer really moved the model
 
 

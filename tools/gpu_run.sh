@@ -41,8 +41,9 @@ for step in "$@"; do
   echo "== $step" >&2
   case $name in
     tests)
-      timeout -k 10 900 python -u -m pytest -q -rs --maxfail 20 --timeout 300 --timeout-method thread \
-        ${arg:-tests} -m gpu > "$out/pytest_gpu.log" 2>&1 ;;
+      # eval: ARGS may quote a -k expression, e.g. 'tests:-k "a or b" tests/test_x.py'
+      eval timeout -k 10 900 python -u -m pytest -q -rs --maxfail 20 --timeout 300 --timeout-method thread \
+        "${arg:-tests}" -m gpu > "$out/pytest_gpu.log" 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 ;;
     bench)
