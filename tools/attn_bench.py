@@ -39,7 +39,8 @@ def run(P, T, heads, drop, iters=5, bits=False, variant=1):
 
 
 variants = [int(v) for v in sys.argv[1:]] or [1, 2]
-for P, T in ((640, 513), (640, 393)):
+Ts = [int(t) for t in os.environ.get("ATTN_SHAPES", "513,393").split(",")]  # e.g. 513,512,393,384
+for P, T in [(640, t) for t in Ts]:
     for drop, bits in ((False, False), (True, True)):
         for var in variants:
             print(json.dumps({"P": P, "T": T, "drop": drop, "bits": bits, "variant": var,

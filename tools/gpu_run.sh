@@ -55,7 +55,7 @@ for step in "$@"; do
       for v in "$arg" tree "$arg" tree; do
         with_lib "$v"
         case $name in
-          attn-ab) kstats "$out/attn_${v}_stats.csv" tools/attn_bench.py 1 ;;
+          attn-ab) kstats "$out/attn_${v}_stats.csv" tools/attn_bench.py 1; timeout -k 10 200 python3 tools/attn_bench.py 1 >> "$out/attn_${v}.log" 2>&1 ;;
           epi-ab) timeout -k 10 200 python3 tools/gemm_epi_bench.py 4 >> "$out/epi_$v.log" 2>&1 ;;
           bench-ab) timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 $short --fwd-steps 0 \
                       >> "$out/bench_$v.log" 2>&1 ;;
