@@ -188,6 +188,18 @@ mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, mmseq_rows x
                                  mmseq_rows yl, float* mean, float* rstd, mmseq_dtype x_dtype,
                                  mmseq_dtype y_dtype, const mmseq_dropout* drop_y,
                                  mmseq_stream stream);
+/* layernorm_bwd_mxfp8: mmseq_layernorm_bwd (bf16, cols 256..1024 in steps of 256) that also writes
+ *  the gradient the next data-gradient GEMM reads — dx_drop when given, else dx (with dres) — in
+ *  MX-fp8 (mmseq_quant_mxfp8 layout, bit-identical to quantising it; q_scales must be zeroed by the
+ *  caller for the padding rows): config 5's fp8 dgrad (lxrt/modeling.py:428-439,488-493). */
+mmseq_status mmseq_layernorm_bwd_mxfp8(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                       const void* x, mmseq_rows xl, const float* mean,
+                                       const float* rstd, const float* gamma, void* dx,
+                                       mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                       float* dgamma, float* dbeta, float* workspace,
+                                       const mmseq_dropout* drop_dy, void* dx_drop,
+                                       const mmseq_dropout* drop_dx, void* q, int64_t ldq,
+                                       void* q_scales, mmseq_stream stream);
 /* layernorm_fwd_mxfp8: bf16 LayerNorm (no dropout) that also writes its output in the MX-fp8 format
  *  of mmseq_quant_mxfp8 (q [rows][ldq] e4m3 + packed scales, bit-identical to quantising the bf16
  *  output), the A operand of the next fp8 GEMM (BASELINE config 5: QKV and FC1 after the LNs of
@@ -428,7 +440,8 @@ mmseq_status mmseq_gemm_mxfp8_q8(int M, int N, int K, const void* A, int64_t lda
  *  (no resid / drop) with C (optional) its bf16 copy and aux the pre-activation (FC1: what the
  *  backward reads and FC2's fp8 operand, lxrt/modeling.py:467-493, clip/model.py:208-214).
  *  With dact (and act, nothing else): the dgrad form C = (A B^T) * act'(dact), dact bf16 [M][ldc]
- *  (the backward's fp8 dgrad: dz = dY W * GELU'(z)). The dropout mask is the bf16 GEMM's
+ *  (the backward's fp8 dgrad: dz = dY W * GELU'(z)); with q as well, q / q_scales = its MX-fp8 (the
+ *  next dgrad GEMM's operand) and C the bf16 copy (the weight gradient's operand). The dropout mask is the bf16 GEMM's
  *  (mmseq_gemm) for the same descriptor. K % 256 == 0 and
  *  M, N >= 256 (else MMSEQ_EUNSUPPORTED); ldc, ldr % 8, ldq % 16, 16-byte aligned buffers. */
 mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, int64_t lda,

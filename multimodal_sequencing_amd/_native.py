@@ -95,6 +95,9 @@ _SIGS = {
     "mmseq_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
                                            _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
                                            ctypes.c_int, _dp, _vp, _dp, _vp]),
+    "mmseq_layernorm_bwd_mxfp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows,
+                                                 _vp, _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
+                                                 _dp, _vp, _dp, _vp, _c_i64, _vp, _vp]),
     "mmseq_embed_ln_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 7 + [ctypes.c_float, _vp,
                                                                            _c_i64, _vp, _vp,
                                                                            ctypes.c_int, _dp, _vp]),
@@ -345,6 +348,22 @@ def layernorm_bwd(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres,
                                      _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
                                      _p(dbeta), _p(ws), dt(x), _d(drop_dy), _p(dx_drop),
                                      _d(drop_dx), _stream()), "mmseq_layernorm_bwd")
+
+
+def layernorm_bwd_mxfp8(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl, dgamma,
+                        dbeta, drop_dy=None, dx_drop=None, drop_dx=None):
+    """layernorm_bwd (bf16) whose dgrad-GEMM operand (dx_drop, else dx) also leaves in MX-fp8
+    (mmseq_layernorm_bwd_mxfp8) -> MXFP8 [nrows][cols]."""
+    ws = torch.empty(lib().mmseq_layernorm_bwd_workspace(nrows, cols), dtype=torch.float32,
+                     device=x.device)
+    ldq = (cols + 15) // 16 * 16
+    q = torch.empty(nrows, ldq, dtype=torch.uint8, device=x.device)
+    sc = torch.zeros(lib().mmseq_mxfp8_scale_bytes(nrows, cols), dtype=torch.uint8, device=x.device)
+    _check(lib().mmseq_layernorm_bwd_mxfp8(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
+                                           _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
+                                           _p(dbeta), _p(ws), _d(drop_dy), _p(dx_drop), _d(drop_dx),
+                                           _p(q), ldq, _p(sc), _stream()), "mmseq_layernorm_bwd_mxfp8")
+    return MXFP8(q, sc, nrows, cols)
 
 
 def embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gamma, beta, eps, joint, ld_pair, mean, rstd,

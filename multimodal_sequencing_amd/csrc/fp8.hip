@@ -386,8 +386,9 @@ extern "C" mmseq_status mmseq_gemm_mxfp8(int M, int N, int K, const void* A, int
 // with aux = the pre-activation, or, with q, the MX-fp8 output q + q_scales (and C then its bf16
 // copy, aux the pre-activation; no residual / dropout): the MLP's FC1 writes what the backward reads
 // (bf16 GELU output and pre-activation) and FC2's fp8 operand in one epilogue; or, with dact, the
-// dgrad form C = (A B^T) * act'(dact). The 256 x 256 8-phase F8 schedule only (K % 256 == 0, M and
-// N >= 256); otherwise MMSEQ_EUNSUPPORTED.
+// dgrad form C = (A B^T) * act'(dact) (with q: its MX-fp8 copy for the next dgrad GEMM too, C then
+// the bf16 copy the weight gradient reads). The 256 x 256 8-phase F8 schedule only (K % 256 == 0,
+// M and N >= 256); otherwise MMSEQ_EUNSUPPORTED.
 extern "C" mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, int64_t lda,
                                             const void* a_scales, const void* B, int64_t ldb,
                                             const void* b_scales, void* C, int64_t ldc,
@@ -399,7 +400,7 @@ extern "C" mmseq_status mmseq_gemm_mxfp8_ex(int M, int N, int K, const void* A, 
   MMSEQ_REQUIRE(A && B && a_scales && b_scales && (C || q), "gemm_mxfp8_ex: null buffer");
   MMSEQ_REQUIRE(!q == !q_scales, "gemm_mxfp8_ex: q and q_scales go together");
   MMSEQ_REQUIRE(!aux || act, "gemm_mxfp8_ex: aux needs an activation");
-  MMSEQ_REQUIRE(!dact || (act && !aux && !resid && !bias && !q && !(drop && drop->p > 0.f)),
+  MMSEQ_REQUIRE(!dact || (act && !aux && !resid && !bias && !(drop && drop->p > 0.f)),
                 "gemm_mxfp8_ex: dact (dgrad) takes an activation and nothing else");
   MMSEQ_REQUIRE(act == 0 || act == MMSEQ_ACT_GELU_ERF || act == MMSEQ_ACT_QUICKGELU,
                 "gemm_mxfp8_ex: act");

@@ -30,12 +30,13 @@ __device__ __forceinline__ void st8(us* p, const float* v) {
 // one 16-byte operand per call: dact (BWD), else the residual, else C (accumulate); the host
 // never sends the 256 kernels a residual together with accumulate
 struct EpiIn { u16x8 x; };
-template <bool BWD>
+template <bool BWD, bool Q8 = false>
 __device__ __forceinline__ EpiIn epi8_load(const GemmArgs& a, int m, int n) {
   EpiIn in;
   in.x = (u16x8){0, 0, 0, 0, 0, 0, 0, 0};
   if (m >= a.M || n >= a.N) return in;
-  const int64_t off = (int64_t)m * a.ldc + n;
+  // MX-fp8 output (Q8): ldc is the fp8 output's row stride, dact has the bf16 copy's (ldcb)
+  const int64_t off = (int64_t)m * (Q8 ? a.ldcb : a.ldc) + n;
   if (BWD) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.dact) + off);
   else if (a.resid) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.resid) + (int64_t)m * a.ldr + n);
   else if (a.accumulate) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.C) + off);
@@ -141,9 +142,12 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
 // same row (g = 0..3: 32 columns = one E8M0 block) for the block's amax, then quantise like
 // mmseq_quant_mxfp8 (bit-identical to it on the bf16 output): 8 e4m3 bytes per lane, the scale
 // byte by lane group 0; rows in [M, M rounded up to 64) get scale 0, as the quantiser writes.
-template <int ACT>
+// BWD (the fp8 dgrad of config 5): the output is (A B^T) * act'(dact) from the dgrad table instead,
+// e.g. dz = dY W2 * GELU'(z), whose MX-fp8 copy is the next dgrad GEMM's operand.
+template <int ACT, bool BWD = false>
 __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, f32x4 lo, f32x4 hi,
-                                        const EpiBias& bias) {
+                                        const EpiBias& bias, const EpiIn* din = nullptr,
+                                        const float MMSEQ_LDS* dtab = nullptr) {
   float v[8];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -152,13 +156,18 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
   }
   const bool in = m < a.M && n < a.N;
   const int64_t offb = (int64_t)m * a.ldcb + n;
-  if (ACT && a.aux && in) st8(reinterpret_cast<us*>(a.aux) + offb, v);  // training: pre-activation
-  if (ACT == MMSEQ_ACT_GELU_ERF) {
+  if (BWD) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
-  } else if (ACT) {
+    for (int r = 0; r < 8; ++r) v[r] *= dtab[dtab_index(din->x[r])];
+  } else {
+    if (ACT && a.aux && in) st8(reinterpret_cast<us*>(a.aux) + offb, v);  // training: pre-activation
+    if (ACT == MMSEQ_ACT_GELU_ERF) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
+      for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
+    } else if (ACT) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
+    }
   }
   float amax = 0.f;
 #pragma unroll
@@ -583,7 +592,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
-          in[0][i][t] = epi8_load<BWD>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
+          in[0][i][t] = epi8_load<BWD, Q8>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         if (h + 1 < 4) {
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
-              in[(h + 1) & 1][i][t] = epi8_load<BWD>(a, m0 + wr * 128 + (2 * h + 2 + i) * 16 + ii,
+              in[(h + 1) & 1][i][t] = epi8_load<BWD, Q8>(a, m0 + wr * 128 + (2 * h + 2 + i) * 16 + ii,
                                                      n0 + wc * 64 + 32 * t + 8 * g);
         }
         asm volatile("" ::"v"(in[h & 1][0][0].x), "v"(in[h & 1][0][1].x), "v"(in[h & 1][1][0].x),
@@ -599,10 +608,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-            epi8<ACT, BWD, true, BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                      acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
-                                      t ? bias1 : bias0, dtab);
+          for (int t = 0; t < 2; ++t) {
+            if (Q8 && BWD)  // fp8 dgrad writing the next dgrad's MX-fp8 operand (+ bf16 copy)
+              epi8_q8<ACT, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, g,
+                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], t ? bias1 : bias0,
+                                 &in[h & 1][i][t], dtab);
+            else
+              epi8<ACT, BWD, true, BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                        acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
+                                        t ? bias1 : bias0, dtab);
+          }
       }
     } else if (Q8) {
 #pragma unroll
@@ -1077,8 +1092,9 @@ bool mmseq_gemm256_nt_f8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_
       !a16(a.B) || !a.f8_sa || !a.f8_sb || a.accumulate || !a16(a.C))
     return false;
   if (a.aux && (!a16(a.aux) || !a.act)) return false;
-  // dgrad form: C = (A B^T) * act'(dact) (the activation derivative at the stored pre-activation)
-  if (a.dact && (!a.act || q8 || a.resid || a.aux || a.bias || a.drop.thr || !a16(a.dact))) return false;
+  // dgrad form: C = (A B^T) * act'(dact) (the activation derivative at the stored pre-activation);
+  // with q8_scales the MX-fp8 output (+ its bf16 copy cbf), dact then in cbf's layout (ldcb)
+  if (a.dact && (!a.act || a.resid || a.aux || a.bias || a.drop.thr || !a16(a.dact))) return false;
   // MX-fp8 out: no residual / dropout; its optional bf16 copy and aux share ldcb. bf16 out: the
   // plain epilogue (bias, activation + aux, dropout, residual)
   if (q8 ? (a.N % 32 != 0 || a.ldc % 16 != 0 || a.resid || a.drop.thr ||
@@ -1092,7 +1108,12 @@ bool mmseq_gemm256_nt_f8(const GemmArgs& a, int num_cu, hipStream_t s, hipError_
   const dim3 grid(ntiles < num_cu ? ntiles : num_cu), block(512);
 #define F8_LAUNCH(ACT, XIN, Q8) \
   hipLaunchKernelGGL((gemm256_nt_kernel<ACT, false, XIN, Q8, true>), grid, block, 0, s, a, tn, ntiles, 0)
-  if (a.dact) {
+  if (a.dact && q8) {
+    if (a.act == MMSEQ_ACT_GELU_ERF)
+      hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, true, true, true, true>), grid, block, 0, s, a, tn, ntiles, 0);
+    else
+      hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_QUICKGELU, true, true, true, true>), grid, block, 0, s, a, tn, ntiles, 0);
+  } else if (a.dact) {
     if (a.act == MMSEQ_ACT_GELU_ERF)
       hipLaunchKernelGGL((gemm256_nt_kernel<MMSEQ_ACT_GELU_ERF, true, true, false, true>), grid, block, 0, s, a, tn, ntiles, 0);
     else

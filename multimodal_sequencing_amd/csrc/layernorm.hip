@@ -370,7 +370,10 @@ __global__ __launch_bounds__(256) void ln_fwd16_q8_kernel(int rows, int cols,
 // each half wave walks rows hw, hw + 8, ... with the next row's loads issued before the current
 // row's math; per-block dgamma / dbeta partials -> ws[block][2][cols]
 constexpr int RPB16 = 64;
-template <int NJ, bool DIN, bool DXD>
+// Q8 (config 5's fp8 dgrad): the gradient the next data-gradient GEMM reads (dxd when written, else
+// dx with the residual) also leaves in MX-fp8 (mmseq_quant_mxfp8 of the bf16 values: q [rows][ldq],
+// packed scales; the padding rows' scales are the caller's, zero-initialised)
+template <int NJ, bool DIN, bool DXD, bool Q8 = false>
 __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const us* __restrict__ dy,
                                                        mmseq_rows dyl, const us* __restrict__ x,
                                                        mmseq_rows xl, const float* __restrict__ mean,
@@ -379,7 +382,9 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const
                                                        us* __restrict__ dx, mmseq_rows dxl,
                                                        const us* __restrict__ dres, mmseq_rows dresl,
                                                        float* __restrict__ ws, Drop din,
-                                                       us* __restrict__ dxd, Drop dout) {
+                                                       us* __restrict__ dxd, Drop dout,
+                                                       uint8_t* __restrict__ q8 = nullptr,
+                                                       int64_t ldq = 0, uint8_t* __restrict__ q8s = nullptr) {
   __shared__ float red[4][2][NJ * 256];
   const int l = threadIdx.x & 31, hw = threadIdx.x >> 5;
   float pg[NJ][8], pb[NJ][8];
@@ -446,12 +451,14 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const
         const float dd = DIN ? d[e] * dm[e] : d[e];
         o[e] = rs * (dd * g8[e] - s1 - (xv[e] - mu) * rs * s2);
       }
+      u16x8 qsrc;
       if (DXD) {
         float od[8], dm2[8];
         drop_mul_pairs<4>(dout, (uint64_t)r * cols + c, dm2);
 #pragma unroll
         for (int e = 0; e < 8; ++e) od[e] = o[e] * dm2[e];
-        *reinterpret_cast<u16x8*>(dxd + row_off(dxl, r) + c) = pack8(od);
+        qsrc = pack8(od);
+        *reinterpret_cast<u16x8*>(dxd + row_off(dxl, r) + c) = qsrc;
       }
       if (drr) {
         float t[8];
@@ -459,7 +466,37 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] += t[e];
       }
-      *reinterpret_cast<u16x8*>(dxr + c) = pack8(o);
+      const u16x8 ob = pack8(o);
+      *reinterpret_cast<u16x8*>(dxr + c) = ob;
+      if (Q8) {  // 32-column block = lanes l .. l + 3 (l & ~3): amax by two lane swaps
+        if (!DXD) qsrc = ob;
+        float qv[8], amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          qv[e] = bf2f(qsrc[e]);
+          amax = fmaxf(amax, fabsf(qv[e]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+        int ex = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
+        ex = max(-127, min(127, ex - 8));
+        const float inv = ldexpf(1.f, -ex);
+        if ((l & 3) == 0)
+          q8s[((r >> 6) * (cols >> 5) + (c >> 5)) * 64 + (r & 15) * 4 + ((r >> 4) & 3)] = (uint8_t)(ex + 127);
+        uint32_t w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float s0 = fminf(448.f, fmaxf(-448.f, qv[4 * h] * inv));
+          const float s1 = fminf(448.f, fmaxf(-448.f, qv[4 * h + 1] * inv));
+          const float s2 = fminf(448.f, fmaxf(-448.f, qv[4 * h + 2] * inv));
+          const float s3 = fminf(448.f, fmaxf(-448.f, qv[4 * h + 3] * inv));
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+          pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+          w[h] = (uint32_t)pk;
+        }
+        typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+        *reinterpret_cast<u32x2*>(q8 + r * ldq + c) = (u32x2){w[0], w[1]};
+      }
     }
   }
   // deterministic cross-half-wave reduction in two LDS rounds (keeps LDS at 8 KB per 256 columns)
@@ -560,14 +597,14 @@ extern "C" int64_t mmseq_layernorm_bwd_workspace(int rows, int cols) {
   return (int64_t)nb * 2 * cols + mmseq_reduce_extra(nb, 2 * cols);
 }
 
-extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
-                                            const void* x, mmseq_rows xl, const float* mean,
-                                            const float* rstd, const float* gamma, void* dx,
-                                            mmseq_rows dxl, const void* dres, mmseq_rows dresl,
-                                            float* dgamma, float* dbeta, float* workspace,
-                                            mmseq_dtype dtype, const mmseq_dropout* drop_dy,
-                                            void* dx_drop, const mmseq_dropout* drop_dx,
-                                            mmseq_stream stream) {
+static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                       const void* x, mmseq_rows xl, const float* mean,
+                                       const float* rstd, const float* gamma, void* dx,
+                                       mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                       float* dgamma, float* dbeta, float* workspace,
+                                       mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                       void* dx_drop, const mmseq_dropout* drop_dx, void* q,
+                                       int64_t ldq, void* q_scales, mmseq_stream stream) {
   MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 2048, "layernorm_bwd: cols must be in (0, 2048]");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "layernorm_bwd: null buffer");
   if (rows == 0) return MMSEQ_OK;
@@ -586,9 +623,18 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
     const bool di = din.thr != 0, dd = dx_drop != nullptr;
 #define LNB16K(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B>), dim3(nb16), dim3(256), 0, s, rows, \
                     cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,         \
-                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dout)
+                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dout, nullptr, 0, nullptr)
+#define LNB16Q(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B, true>), dim3(nb16), dim3(256), 0, s, \
+                    rows, cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,   \
+                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dout, (uint8_t*)q, ldq,       \
+                    (uint8_t*)q_scales)
 #define LNB16(NJ)                                           \
-  if (di && dd) LNB16K(NJ, true, true);                     \
+  if (q) {                                                  \
+    if (di && dd) LNB16Q(NJ, true, true);                   \
+    else if (di) LNB16Q(NJ, true, false);                   \
+    else if (dd) LNB16Q(NJ, false, true);                   \
+    else LNB16Q(NJ, false, false);                          \
+  } else if (di && dd) LNB16K(NJ, true, true);              \
   else if (di) LNB16K(NJ, true, false);                     \
   else if (dd) LNB16K(NJ, false, true);                     \
   else LNB16K(NJ, false, false);                            \
@@ -597,12 +643,14 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
       case 1: LNB16(1); case 2: LNB16(2); case 3: LNB16(3); case 4: LNB16(4);
     }
 #undef LNB16
+#undef LNB16Q
 #undef LNB16K
     mmseq_status st = mmseq_check_launch("layernorm_bwd");
     if (st) return st;
     if (dgamma || dbeta) return ln_reduce_partials(nb16, cols, workspace, dgamma, dbeta, s);
     return MMSEQ_OK;
   }
+  if (q) return mmseq_set_error(MMSEQ_EUNSUPPORTED, "layernorm_bwd_mxfp8: bf16, cols 256..1024 (x256), 16-byte rows");
 #define LNBJ(T, V, J)                                                                             \
   hipLaunchKernelGGL((ln_bwd_kernel<T, V, J>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy, \
                      dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl,   \
@@ -620,6 +668,34 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
   if (st) return st;
   if (dgamma || dbeta) return ln_reduce_partials(nb, cols, workspace, dgamma, dbeta, s);
   return MMSEQ_OK;
+}
+
+extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                            const void* x, mmseq_rows xl, const float* mean,
+                                            const float* rstd, const float* gamma, void* dx,
+                                            mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                            float* dgamma, float* dbeta, float* workspace,
+                                            mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                            void* dx_drop, const mmseq_dropout* drop_dx,
+                                            mmseq_stream stream) {
+  return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
+                            dgamma, dbeta, workspace, dtype, drop_dy, dx_drop, drop_dx, nullptr, 0,
+                            nullptr, stream);
+}
+
+extern "C" mmseq_status mmseq_layernorm_bwd_mxfp8(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                                  const void* x, mmseq_rows xl, const float* mean,
+                                                  const float* rstd, const float* gamma, void* dx,
+                                                  mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                                  float* dgamma, float* dbeta, float* workspace,
+                                                  const mmseq_dropout* drop_dy, void* dx_drop,
+                                                  const mmseq_dropout* drop_dx, void* q, int64_t ldq,
+                                                  void* q_scales, mmseq_stream stream) {
+  MMSEQ_REQUIRE(q && q_scales && ldq >= cols && ldq % 16 == 0 && ((uintptr_t)q & 15) == 0,
+                "layernorm_bwd_mxfp8: q / ldq");
+  return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
+                            dgamma, dbeta, workspace, MMSEQ_BF16, drop_dy, dx_drop, drop_dx, q, ldq,
+                            q_scales, stream);
 }
 
 extern "C" mmseq_status mmseq_layernorm_fwd_mxfp8(int rows, int cols, const void* x, mmseq_rows xl,

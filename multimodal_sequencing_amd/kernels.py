@@ -157,14 +157,15 @@ def _mlp_fwd(st, x, Wi, bi, act, Wo, bo, resid, lin, xq=None):
     return lin(lin(x, Wi, bias=bi, act=act), Wo, bias=bo, resid=resid)
 
 
-def _dgrad8(dy, st, WT, resid=None, act=0, dact=None):
-    """dx = dy W (+ resid) or (dy W) * act'(dact) on the fp8 MFMA: dy quantised to MX-fp8 here,
-    the transposed weight shadow WT [in][out] once per store version (config 5, dgrad=True)."""
+def _dgrad8(dy, st, WT, resid=None, act=0, dact=None, dyq=None, q8=False):
+    """dx = dy W (+ resid) or (dy W) * act'(dact) on the fp8 MFMA: dy's MX-fp8 copy from its producer
+    (dyq) or quantised here, the transposed weight shadow WT [in][out] once per store version
+    (config 5, dgrad=True). q8: also return the output's MX-fp8 copy (the next dgrad's operand)."""
     R = dy.numel() // dy.shape[-1]
     out = torch.empty(R, WT.shape[0], device=dy.device, dtype=dy.dtype)
-    N.gemm_mxfp8_ex(N.quant_mxfp8(dy.view(R, -1)), _fp8_weight(st, WT), out, act=act, dact=dact,
-                    resid=resid)
-    return out
+    q = N.gemm_mxfp8_ex(dyq if dyq is not None else N.quant_mxfp8(dy.view(R, -1)),
+                        _fp8_weight(st, WT), out, act=act, dact=dact, resid=resid, q8=q8)
+    return (out, q) if q8 else out
 
 
 def _dgrad(dy, WT, resid=None, act=0, dact=None, out=None):
@@ -357,24 +358,28 @@ class BertLayerFn(torch.autograd.Function):
         # the residual branch keeps the unmasked one (ds2)
         ds2 = torch.empty_like(dy)
         ds2d = torch.empty_like(dy) if d_out is not None else ds2
-        N.layernorm_bwd(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
-                        None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b),
-                        dx_drop=ds2d if d_out is not None else None, drop_dx=d_out)
-        f8 = getattr(ctx, "f8dg", False)
-        dg = (lambda d, WT, **kw: _dgrad8(d, st, WT, **kw)) if f8 else _dgrad
+        f8 = getattr(ctx, "f8dg", False)  # fp8 dgrad: the LN backwards also write the MX-fp8 operand
+        lnb = N.layernorm_bwd_mxfp8 if f8 else N.layernorm_bwd
+        ds2q = lnb(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
+                   None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b),
+                   dx_drop=ds2d if d_out is not None else None, drop_dx=d_out)
         _wgrad(ds2d, gact, st.g(L.out_w), st.g(L.out_b))
-        dz = dg(ds2d, st.wt(L.out_w), act=GELU, dact=z)
+        dzq = None  # fp8 dgrad: FC2's dgrad epilogue writes FC1's dgrad operand in MX-fp8 as well
+        if f8:
+            dz, dzq = _dgrad8(ds2d, st, st.wt(L.out_w), act=GELU, dact=z, dyq=ds2q, q8=True)
+        else:
+            dz = _dgrad(ds2d, st.wt(L.out_w), act=GELU, dact=z)
         del ds2d
         _wgrad(dz, h1, st.g(L.i_w), st.g(L.i_b))
-        dh1 = dg(dz, st.wt(L.i_w), resid=ds2)
-        del dz
+        dh1 = _dgrad8(dz, st, st.wt(L.i_w), resid=ds2, dyq=dzq) if f8 else _dgrad(dz, st.wt(L.i_w), resid=ds2)
+        del dz, dzq
         ds1 = torch.empty_like(dy)
         ds1d = torch.empty_like(dy) if d_o is not None else ds1
-        N.layernorm_bwd(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
-                        None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
-                        dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
+        ds1q = lnb(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
+                   None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
+                   dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
         _wgrad(ds1d, o, st.g(L.o_w), st.g(L.o_b))
-        do = dg(ds1d, st.wt(L.o_w))
+        do = _dgrad8(ds1d, st, st.wt(L.o_w), dyq=ds1q) if f8 else _dgrad(ds1d, st.wt(L.o_w))
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
@@ -383,7 +388,8 @@ class BertLayerFn(torch.autograd.Function):
         ctx.kbits = None
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         st.grad_ready(L.span)
-        dx = dg(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
+        dx = _dgrad8(dqkv, st, st.wt(L.qkv_w[0]), resid=ds1) if f8 else \
+            _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None, None
 
 
@@ -487,15 +493,21 @@ class VitBlockFn(torch.autograd.Function):
         f8 = getattr(ctx, "f8dg", False)
         dg = (lambda d, WT, **kw: _dgrad8(d, st, WT, **kw)) if f8 else _dgrad
         _wgrad(dx2, gact, st.g(L.proj_w), st.g(L.proj_b))
-        dz = dg(dx2, st.wt(L.proj_w), act=QGELU, dact=z)
+        dzq = None
+        if f8:
+            dz, dzq = _dgrad8(dx2, st, st.wt(L.proj_w), act=QGELU, dact=z, q8=True)
+        else:
+            dz = _dgrad(dx2, st.wt(L.proj_w), act=QGELU, dact=z)
         _wgrad(dz, hn2, st.g(L.fc_w), st.g(L.fc_b))
-        dhn2 = dg(dz, st.wt(L.fc_w))
+        dhn2 = _dgrad8(dz, st, st.wt(L.fc_w), dyq=dzq) if f8 else _dgrad(dz, st.wt(L.fc_w))
+        del dzq
         del dz
         dx1 = torch.empty_like(h)
-        N.layernorm_bwd(R, W, dhn2, _rows(W), x1, _rows(W), m2, r2, st.f32(L.ln2_w), dx1, _rows(W),
-                        dx2, _rows(W), st.g(L.ln2_w), st.g(L.ln2_b))
+        dx1q = (N.layernorm_bwd_mxfp8 if f8 else N.layernorm_bwd)(
+            R, W, dhn2, _rows(W), x1, _rows(W), m2, r2, st.f32(L.ln2_w), dx1, _rows(W), dx2, _rows(W),
+            st.g(L.ln2_w), st.g(L.ln2_b))
         _wgrad(dx1, o, st.g(L.out_w), st.g(L.out_b))
-        do = dg(dx1, st.wt(L.out_w))
+        do = dg(dx1, st.wt(L.out_w), dyq=dx1q) if f8 else _dgrad(dx1, st.wt(L.out_w))
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=h.device)
         N.attn_bwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,

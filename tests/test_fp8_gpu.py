@@ -319,6 +319,12 @@ def test_gemm_mxfp8_ex_dgrad_epilogue(rows, Nn, K, act):
     N.gemm_mxfp8(qa, qb, plain)
     got = torch.empty_like(plain)
     N.gemm_mxfp8_ex(qa, qb, got, act=act, dact=z)
+    # with q8: the same bf16 output and its MX-fp8 copy (bit-identical to quantising it)
+    got2 = torch.empty_like(plain)
+    q = N.gemm_mxfp8_ex(qa, qb, got2, act=act, dact=z, q8=True)
+    assert torch.equal(got2, got)
+    want = N.quant_mxfp8(got)
+    assert torch.equal(q.q[:, :Nn], want.q[:, :Nn]) and torch.equal(q.scales, want.scales)
     zf = z.float()
     if act == 1:
         d = 0.5 * (1 + torch.erf(zf / math.sqrt(2))) + zf * torch.exp(-0.5 * zf * zf) / math.sqrt(2 * math.pi)
@@ -326,6 +332,39 @@ def test_gemm_mxfp8_ex_dgrad_epilogue(rows, Nn, K, act):
         sg = torch.sigmoid(1.702 * zf)
         d = sg + 1.702 * zf * sg * (1 - sg)
     torch.testing.assert_close(got.float(), plain.float() * d, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("rows,cols,mode", [(300, 1024, "drop"), (513, 768, "res"), (64, 256, "plain")])
+def test_layernorm_bwd_mxfp8_matches_bwd_then_quant(rows, cols, mode):
+    """mmseq_layernorm_bwd_mxfp8 (config 5's fp8 dgrad): dx / dx_drop / dgamma / dbeta identical to
+    mmseq_layernorm_bwd, and the MX-fp8 copy of the dgrad operand (dx_drop, else dx with the
+    residual) bit-identical to quantising it."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, device=DEV, generator=g) * 2 + 0.5).bfloat16()
+    dy = torch.randn(rows, cols, device=DEV, generator=g).bfloat16()
+    gamma = 1 + 0.1 * torch.randn(cols, device=DEV, generator=g)
+    beta = torch.zeros(cols, device=DEV)
+    m, r = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    N.layernorm_fwd(rows, cols, x, N.rows(cols), gamma, beta, 1e-5, torch.empty_like(x), N.rows(cols), m, r)
+    dres = torch.randn(rows, cols, device=DEV, generator=g).bfloat16() if mode == "res" else None
+    d = N.drop(0.1, 9, 17) if mode == "drop" else None
+    outs = []
+    for fn in (N.layernorm_bwd, N.layernorm_bwd_mxfp8):
+        dx = torch.empty_like(x)
+        dxd = torch.empty_like(x) if d is not None else None
+        dgm, dbt = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+        q = fn(rows, cols, dy, N.rows(cols), x, N.rows(cols), m, r, gamma, dx, N.rows(cols), dres,
+               N.rows(cols), dgm, dbt, dx_drop=dxd, drop_dx=d)
+        outs.append((dx, dxd, dgm, dbt, q))
+    (dx0, dxd0, g0, b0, _), (dx1, dxd1, g1, b1, q) = outs
+    assert torch.equal(dx1, dx0) and torch.equal(g1, g0) and torch.equal(b1, b0)
+    tgt = dx0
+    if d is not None:
+        assert torch.equal(dxd1, dxd0)
+        tgt = dxd0
+    want = N.quant_mxfp8(tgt)
+    assert torch.equal(q.q[:, :cols], want.q[:, :cols]) and torch.equal(q.scales, want.scales)
 
 
 def _c5_pair(steps_lr=1e-4):
