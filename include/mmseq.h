@@ -147,6 +147,16 @@ mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld
                             int64_t ld_dout, const float* lse, float* delta, void* dqkv,
                             int64_t ld_dqkv, mmseq_dtype dtype, const mmseq_dropout* drop,
                             const uint64_t* keep_bits, int variant, mmseq_stream stream);
+/* attn_bwd_mxfp8: the bf16 fast backward (variant 1) over the packed Q|K|V layout (q_off 0, k_off
+ *  heads*64, v_off 2*heads*64) that also writes dQ|dK|dV in MX-fp8 (q8 [P*T][ldq8] e4m3 + packed
+ *  scales of the [P*T][3*heads*64] operand, bit-identical to quantising dqkv; padding-row scales
+ *  zeroed by the caller): the QKV data-gradient GEMM's operand in config 5's fp8 dgrad. */
+mmseq_status mmseq_attn_bwd_mxfp8(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                  const float* key_bias, float scale, const void* out,
+                                  int64_t ld_out, const void* dout, int64_t ld_dout,
+                                  const float* lse, float* delta, void* dqkv, int64_t ld_dqkv,
+                                  const mmseq_dropout* drop, const uint64_t* keep_bits, void* q8,
+                                  int64_t ldq8, void* q8_scales, mmseq_stream stream);
 /* Attention-probability dropout keep-mask cache (bf16 fast kernels): with keep_bits != NULL the
  * forward also stores its counter-based keep mask as bits (word [(p*heads + h)*T + q][kt] for key
  * tile kt < round_up_even(ceil(T/64)); key 64*kt + j at bit ((j >> 2) & 3) * 16 + (j >> 4) * 4 +

@@ -81,6 +81,10 @@ _SIGS = {
                                                            _c_i64, _vp, _vp, _vp, _c_i64,
                                                            ctypes.c_int, _dp, _vp, ctypes.c_int,
                                                            _vp]),
+    "mmseq_attn_bwd_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, ctypes.c_float,
+                                                                 _vp, _c_i64, _vp, _c_i64, _vp, _vp,
+                                                                 _vp, _c_i64, _dp, _vp, _vp, _c_i64,
+                                                                 _vp, _vp]),
     "mmseq_small_attn_fwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 4 + [ctypes.c_float, _vp,
                                                                              _vp, _dp, _vp]),
     "mmseq_small_attn_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 5 + [ctypes.c_float, _vp,
@@ -575,6 +579,21 @@ def attn_fwd_mxfp8(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scal
                                       _p(key_bias), scale, _p(lse), _p(q), q.stride(0), _p(sc),
                                       _stream()), "mmseq_attn_fwd_mxfp8")
     return MXFP8(q, sc, rows_, cols)
+
+
+def attn_bwd_mxfp8(P, T, heads, qkv, key_bias, scale, out, dout, lse, delta, dqkv, drop=None,
+                   keep_bits=None):
+    """attn_bwd (bf16 fast kernels, packed Q|K|V) that also returns dQ|dK|dV in MX-fp8
+    (mmseq_attn_bwd_mxfp8): the QKV dgrad GEMM's operand in config 5's fp8 dgrad."""
+    H = heads * 64
+    rows_ = P * T
+    q = torch.empty(rows_, (3 * H + 15) // 16 * 16, dtype=torch.uint8, device=qkv.device)
+    sc = torch.zeros(lib().mmseq_mxfp8_scale_bytes(rows_, 3 * H), dtype=torch.uint8, device=qkv.device)
+    _check(lib().mmseq_attn_bwd_mxfp8(P, T, heads, _p(qkv), qkv.stride(0), _p(key_bias), scale, _p(out),
+                                      out.stride(0), _p(dout), dout.stride(0), _p(lse), _p(delta),
+                                      _p(dqkv), dqkv.stride(0), _d(drop), _p(keep_bits), _p(q),
+                                      q.stride(0), _p(sc), _stream()), "mmseq_attn_bwd_mxfp8")
+    return MXFP8(q, sc, rows_, 3 * H)
 
 
 def attn_fwd_mxfp8_dual(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,

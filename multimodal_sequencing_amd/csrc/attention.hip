@@ -576,6 +576,40 @@ __device__ __forceinline__ float xlane_sum4(float v) {
   const auto r32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
   return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
 }
+
+// MX-fp8 copy of one head's 64 gradient columns of a row of dQ|dK|dV (the backward's Q8 output for
+// config 5's fp8 QKV dgrad): v4[d][r] * mul is column col0 + 16 d + 4 g + r; 32-column block b holds
+// d = 2b, 2b + 1 of the four lanes g of the row, quantised like mmseq_quant_mxfp8 of the bf16 values
+// (the layout of the packed [rows][3 * heads * 64] operand; padding-row scales zeroed by the host)
+__device__ __forceinline__ void q8_head_row(const AttnArgs& a, int64_t row, int col0, const f32x4* v4,
+                                            float mul, int g) {
+  const int KB = 6 * a.heads;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    float v[8], amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = bf2f(f2bf(v4[2 * b + (e >> 2)][e & 3] * mul));
+      amax = fmaxf(amax, fabsf(v[e]));
+    }
+    amax = xlane_max4(amax);
+    int ex = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
+    ex = max(-127, min(127, ex - 8));
+    const float sc = ldexpf(1.f, -ex);
+    if (g == 0)
+      a.q8s[((row >> 6) * KB + (col0 >> 5) + b) * 64 + (row & 15) * 4 + ((row >> 4) & 3)] = (uint8_t)(ex + 127);
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd) {
+      const float s0 = fminf(448.f, fmaxf(-448.f, v[4 * dd] * sc));
+      const float s1 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 1] * sc));
+      const float s2 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 2] * sc));
+      const float s3 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 3] * sc));
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+      *reinterpret_cast<int*>(a.q8 + row * a.ldq8 + col0 + (2 * b + dd) * 16 + 4 * g) = pk;
+    }
+  }
+}
 // A operand of all-ones (bf16 1.0): mma(ONES, P, acc) adds each query column's sum of P to all
 // four of its accumulator rows
 __device__ __forceinline__ bf16x8_t bf16_ones() {
@@ -1422,6 +1456,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
                             ((int64_t)p * T + q) * a.ld_dqkv + a.q_off + h * 64 + 4 * g;
 #pragma unroll
       for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(dqp + d * 16, dq[grp][d] * a.scale);
+      if (a.q8) q8_head_row(a, (int64_t)p * T + q, (int)a.q_off + h * 64, dq[grp], a.scale, g);
     }
   }
 }
@@ -1732,6 +1767,10 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
           Vec4<unsigned short>::st(dkp + d * 16, dkt[d] * a.scale);
           Vec4<unsigned short>::st(dvp + d * 16, dvt[d]);
         }
+        if (a.q8) {
+          q8_head_row(a, (int64_t)p * T + key, (int)a.k_off + h * 64, dkt, a.scale, g);
+          q8_head_row(a, (int64_t)p * T + key, (int)a.v_off + h * 64, dvt, 1.f, g);
+        }
       }
     }
   }
@@ -1747,6 +1786,10 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
       for (int d = 0; d < 4; ++d) {
         Vec4<unsigned short>::st(dkp + d * 16, dk[grp][d] * a.scale);
         Vec4<unsigned short>::st(dvp + d * 16, dv[grp][d]);
+      }
+      if (a.q8) {
+        q8_head_row(a, (int64_t)p * T + key, (int)a.k_off + h * 64, dk[grp], a.scale, g);
+        q8_head_row(a, (int64_t)p * T + key, (int)a.v_off + h * 64, dv[grp], 1.f, g);
       }
     }
   }
@@ -1843,14 +1886,14 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   return mmseq_check_launch("attn_fwd");
 }
 
-extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
-                                       int64_t q_off, int64_t k_off, int64_t v_off,
-                                       const float* key_bias, float scale, const void* out,
-                                       int64_t ld_out, const void* dout, int64_t ld_dout,
-                                       const float* lse, float* delta, void* dqkv,
-                                       int64_t ld_dqkv, mmseq_dtype dtype,
-                                       const mmseq_dropout* drop, const uint64_t* keep_bits,
-                                       int variant, mmseq_stream stream) {
+static mmseq_status attn_bwd_impl(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                  int64_t q_off, int64_t k_off, int64_t v_off,
+                                  const float* key_bias, float scale, const void* out,
+                                  int64_t ld_out, const void* dout, int64_t ld_dout,
+                                  const float* lse, float* delta, void* dqkv, int64_t ld_dqkv,
+                                  mmseq_dtype dtype, const mmseq_dropout* drop,
+                                  const uint64_t* keep_bits, int variant, void* q8, int64_t ldq8,
+                                  void* q8_scales, mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   const int ve = dtype == MMSEQ_BF16 ? 8 : 4;
@@ -1864,6 +1907,9 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
   a.out = out; a.ld_out = ld_out; a.dout = dout; a.ld_dout = ld_dout;
   a.lse = const_cast<float*>(lse); a.delta = delta; a.dqkv = dqkv; a.ld_dqkv = ld_dqkv;
   a.drop = make_drop(drop);
+  a.q8 = reinterpret_cast<uint8_t*>(q8); a.ldq8 = ldq8; a.q8s = reinterpret_cast<uint8_t*>(q8_scales);
+  if (q8 && !(dtype == MMSEQ_BF16 && variant))
+    return mmseq_set_error(MMSEQ_EUNSUPPORTED, "attn_bwd_mxfp8: the bf16 fast kernels only");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t rows = (int64_t)P * T;
   dim3 gd((unsigned)((rows + 3) / 4));
@@ -1905,6 +1951,35 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
     hipLaunchKernelGGL(attn_dq_kernel<float>, grid, dim3(256), 0, s, a);
   }
   return mmseq_check_launch("attn_bwd");
+}
+
+extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                       int64_t q_off, int64_t k_off, int64_t v_off,
+                                       const float* key_bias, float scale, const void* out,
+                                       int64_t ld_out, const void* dout, int64_t ld_dout,
+                                       const float* lse, float* delta, void* dqkv,
+                                       int64_t ld_dqkv, mmseq_dtype dtype,
+                                       const mmseq_dropout* drop, const uint64_t* keep_bits,
+                                       int variant, mmseq_stream stream) {
+  return attn_bwd_impl(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,
+                       dout, ld_dout, lse, delta, dqkv, ld_dqkv, dtype, drop, keep_bits, variant,
+                       nullptr, 0, nullptr, stream);
+}
+
+extern "C" mmseq_status mmseq_attn_bwd_mxfp8(int P, int T, int heads, const void* qkv,
+                                             int64_t ld_qkv, const float* key_bias, float scale,
+                                             const void* out, int64_t ld_out, const void* dout,
+                                             int64_t ld_dout, const float* lse, float* delta,
+                                             void* dqkv, int64_t ld_dqkv,
+                                             const mmseq_dropout* drop, const uint64_t* keep_bits,
+                                             void* q8, int64_t ldq8, void* q8_scales,
+                                             mmseq_stream stream) {
+  const int64_t H = (int64_t)heads * 64;
+  MMSEQ_REQUIRE(q8 && q8_scales && ldq8 >= 3 * H && ldq8 % 16 == 0 && ((uintptr_t)q8 & 15) == 0,
+                "attn_bwd_mxfp8: q8 / ldq8");
+  return attn_bwd_impl(P, T, heads, qkv, ld_qkv, 0, H, 2 * H, key_bias, scale, out, ld_out, dout,
+                       ld_dout, lse, delta, dqkv, ld_dqkv, MMSEQ_BF16, drop, keep_bits, 1, q8, ldq8,
+                       q8_scales, stream);
 }
 
 extern "C" int64_t mmseq_attn_keep_bits_words(int P, int T, int heads) {

@@ -383,12 +383,16 @@ class BertLayerFn(torch.autograd.Function):
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
-        N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
-                   H, do, H, lse, delta, dqkv, 3 * H, drop=d_att, keep_bits=ctx.kbits)
+        if f8:  # dQ|dK|dV also in MX-fp8: the QKV dgrad's operand
+            dqkvq = N.attn_bwd_mxfp8(P, T, heads, qkv, key_bias, 1.0 / math.sqrt(H // heads), o, do,
+                                     lse, delta, dqkv, drop=d_att, keep_bits=ctx.kbits)
+        else:
+            N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias, 1.0 / math.sqrt(H // heads), o,
+                       H, do, H, lse, delta, dqkv, 3 * H, drop=d_att, keep_bits=ctx.kbits)
         ctx.kbits = None
         _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
         st.grad_ready(L.span)
-        dx = _dgrad8(dqkv, st, st.wt(L.qkv_w[0]), resid=ds1) if f8 else \
+        dx = _dgrad8(dqkv, st, st.wt(L.qkv_w[0]), resid=ds1, dyq=dqkvq) if f8 else \
             _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
         return dx, None, None, None, None, None, None, None, None, None
 
@@ -510,10 +514,15 @@ class VitBlockFn(torch.autograd.Function):
         do = dg(dx1, st.wt(L.out_w), dyq=dx1q) if f8 else _dgrad(dx1, st.wt(L.out_w))
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=h.device)
-        N.attn_bwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
-                   do, W, lse, delta, dqkv, 3 * W)
+        dqkvq = None
+        if f8:
+            dqkvq = N.attn_bwd_mxfp8(P, T, heads, qkv, None, 1.0 / math.sqrt(W // heads), o, do, lse,
+                                     delta, dqkv)
+        else:
+            N.attn_bwd(P, T, heads, qkv, 3 * W, 0, W, 2 * W, None, 1.0 / math.sqrt(W // heads), o, W,
+                       do, W, lse, delta, dqkv, 3 * W)
         _wgrad(dqkv, hn, st.g(L.in_w), st.g(L.in_b))
-        dhn = dg(dqkv, st.wt(L.in_w))
+        dhn = dg(dqkv, st.wt(L.in_w), dyq=dqkvq) if f8 else _dgrad(dqkv, st.wt(L.in_w))
         dh = torch.empty_like(h)
         N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
                         dx1, _rows(W), st.g(L.ln1_w), st.g(L.ln1_b))

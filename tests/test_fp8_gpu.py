@@ -367,6 +367,33 @@ def test_layernorm_bwd_mxfp8_matches_bwd_then_quant(rows, cols, mode):
     assert torch.equal(q.q[:, :cols], want.q[:, :cols]) and torch.equal(q.scales, want.scales)
 
 
+@pytest.mark.parametrize("P,T,heads,mode", [(2, 513, 2, "bits"), (1, 393, 16, "none"), (1, 769, 4, "hash")])
+def test_attention_bwd_mxfp8_matches_bwd_then_quant(P, T, heads, mode):
+    """mmseq_attn_bwd_mxfp8 (config 5's fp8 dgrad): dQ|dK|dV identical to mmseq_attn_bwd's (same
+    kernels, T % 128 tail fold included) and its MX-fp8 copy bit-identical to quantising dqkv."""
+    from multimodal_sequencing_amd import _native as N
+    g = torch.Generator(device="cpu").manual_seed(P * T + heads + 11)
+    H = heads * 64
+    qkv = (torch.randn(P * T, 3 * H, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    bias = ((torch.rand(P, T, generator=g) > 0.2).float() - 1).mul(10000.0).to(DEV) if mode == "bits" else None
+    d = N.drop(0.1, 21, 5) if mode != "none" else None
+    kb = N.attn_keep_bits(P, T, heads, DEV).zero_() if mode == "bits" else None
+    out = torch.empty(P * T, H, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(P, heads, T, device=DEV)
+    N.attn_set_fast(1)
+    N.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, lse, drop=d, keep_bits=kb)
+    dout = torch.randn(P * T, H, generator=g).to(DEV, torch.bfloat16)
+    ref = torch.empty_like(qkv)
+    N.attn_bwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, 0.125, out, H, dout, H, lse,
+               torch.empty_like(lse), ref, 3 * H, drop=d, keep_bits=kb)
+    got = torch.full_like(qkv, 3.0)
+    q = N.attn_bwd_mxfp8(P, T, heads, qkv, bias, 0.125, out, dout, lse, torch.empty_like(lse), got,
+                         drop=d, keep_bits=kb)
+    assert torch.equal(got, ref)
+    want = N.quant_mxfp8(ref)
+    assert torch.equal(q.q[:, :3 * H], want.q[:, :3 * H]) and torch.equal(q.scales, want.scales)
+
+
 def _c5_pair(steps_lr=1e-4):
     import json
     import os
