@@ -23,17 +23,26 @@ GROUPS = {
 }
 
 
+def is_f8(name):
+    """gemm256_nt_kernel<ACT, BWD, XIN, Q8, F8>: MX-fp8 instantiations are not the bf16 roofline kernel."""
+    i = name.find("gemm256_nt_kernel<")
+    if i < 0:
+        return False
+    args = name[i + len("gemm256_nt_kernel<"):].split(">")[0].split(",")
+    return len(args) >= 5 and args[4].strip() == "true"
+
+
 def main():
     cus = int(sys.argv[3]) if len(sys.argv) > 3 else 256
     per = collections.defaultdict(lambda: collections.defaultdict(dict))
     for r in csv.DictReader(open(sys.argv[1])):
         for g, key in GROUPS.items():
-            if key in r["Kernel_Name"]:
+            if key in r["Kernel_Name"] and not (g == "gemm256_nt" and is_f8(r["Kernel_Name"])):
                 per[g][r.get("Dispatch_Id") or r.get("Correlation_Id")][r["Counter_Name"]] = \
                     float(r["Counter_Value"])
     out = {"cus": cus, "source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE "
-                                 "SQ_BUSY_CYCLES, bench.py (default config-3 workload) --steps 1 "
-                                 "--warmup 1 via tools/profile_round.sh",
+                                 "SQ_BUSY_CYCLES, bench.py (default config-3 workload, training step only: "
+                                 "--fwd-steps 0) --steps 1 --warmup 1 via tools/profile_round.sh",
            "definition": "MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 4 SIMD * CUs), per dispatch, averaged"}
     for g, disp in per.items():
         utils = []

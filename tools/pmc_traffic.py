@@ -24,13 +24,23 @@ GROUPS = {
 }
 
 
+def is_f8(name):
+    """gemm256_nt_kernel<ACT, BWD, XIN, Q8, F8>: the MX-fp8 operand instantiations (config 5) are
+    not the bf16 roofline kernel."""
+    i = name.find("gemm256_nt_kernel<")
+    if i < 0:
+        return False
+    args = name[i + len("gemm256_nt_kernel<"):].split(">")[0].split(",")
+    return len(args) >= 5 and args[4].strip() == "true"
+
+
 def load(path, counter):
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
         for g, key in GROUPS.items():
-            if key in r["Kernel_Name"]:
+            if key in r["Kernel_Name"] and not (g == "gemm256_nt" and is_f8(r["Kernel_Name"])):
                 per[g].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
@@ -40,7 +50,8 @@ def main():
     write = load(sys.argv[2], "WRITE_SIZE")
     out = {"units": "bytes per launch", "fetch_correction": 2.0,
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
-                     "bench.py (default config-3 workload) --steps 1 --warmup 0 via tools/profile_round.sh"}
+                     "bench.py (default config-3 workload, training step only: --fwd-steps 0) --steps 1 --warmup 0 "
+                     "via tools/profile_round.sh"}
     for g in GROUPS:
         if not fetch.get(g) or not write.get(g):
             continue

@@ -11,7 +11,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 tag=${1:?tag}
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
-args="--no-cpu-baseline --no-config2 --no-config5 --no-rn50 --no-gemm-timer"
+args="--no-cpu-baseline --no-config2 --no-config5 --no-rn50 --no-gemm-timer --fwd-steps 0"  # the training step only
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- \
   python3 bench.py $args --steps 3 --warmup 1 > "$out/kt.log" 2>&1
