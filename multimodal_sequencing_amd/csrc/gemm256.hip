@@ -30,11 +30,11 @@ __device__ __forceinline__ void st8(us* p, const float* v) {
 // one 16-byte operand per call: dact (BWD), else the residual, else C (accumulate); the host
 // never sends the 256 kernels a residual together with accumulate
 struct EpiIn { u16x8 x; };
-template <bool BWD, bool Q8 = false>
+template <bool BWD, bool Q8 = false, bool CHK = true>
 __device__ __forceinline__ EpiIn epi8_load(const GemmArgs& a, int m, int n) {
   EpiIn in;
   in.x = (u16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  if (m >= a.M || n >= a.N) return in;
+  if (CHK && (m >= a.M || n >= a.N)) return in;
   // MX-fp8 output (Q8): ldc is the fp8 output's row stride, dact has the bf16 copy's (ldcb)
   const int64_t off = (int64_t)m * (Q8 ? a.ldcb : a.ldc) + n;
   if (BWD) in.x = *reinterpret_cast<const u16x8*>(reinterpret_cast<const us*>(a.dact) + off);
@@ -88,10 +88,11 @@ __device__ __forceinline__ void dtab_fill(float MMSEQ_LDS* tab) {
   }
 }
 
-template <int ACT, bool BWD, bool XIN, bool DTAB = false>
+// CHK = false: the whole 256 x 256 tile is inside C (no per-call bounds branches)
+template <int ACT, bool BWD, bool XIN, bool DTAB = false, bool CHK = true>
 __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, f32x4 hi, const EpiIn& in,
                                      const EpiBias& bias, const float MMSEQ_LDS* dtab = nullptr) {
-  if (m >= a.M || n >= a.N) return;
+  if (CHK && (m >= a.M || n >= a.N)) return;
   float v[8];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -587,38 +588,49 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
       // h, and each batch is consumed (settled) once, so its wait never covers a store (vmcnt
       // retires in issue order; a consume inside the per-call bounds branches would wait vmcnt(0)).
       // (Three or four batches in flight spill: the fragment registers are not reused here.)
-      EpiIn in[2][2][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          in[0][i][t] = epi8_load<BWD, Q8>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g);
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        if (h + 1 < 4) {
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-              in[(h + 1) & 1][i][t] = epi8_load<BWD, Q8>(a, m0 + wr * 128 + (2 * h + 2 + i) * 16 + ii,
-                                                     n0 + wc * 64 + 32 * t + 8 * g);
-        }
-        asm volatile("" ::"v"(in[h & 1][0][0].x), "v"(in[h & 1][0][1].x), "v"(in[h & 1][1][0].x),
-                     "v"(in[h & 1][1][1].x));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            if (Q8 && BWD)  // fp8 dgrad writing the next dgrad's MX-fp8 operand (+ bf16 copy)
-              epi8_q8<ACT, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, g,
-                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], t ? bias1 : bias0,
-                                 &in[h & 1][i][t], dtab);
-            else
-              epi8<ACT, BWD, true, BWD>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
-                                        acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t],
-                                        t ? bias1 : bias0, dtab);
-          }
+      // Interior tiles (the whole 256 x 256 tile inside C) run without per-call bounds branches.
+#define XIN_EPI(CHK_) \
+      EpiIn in[2][2][2]; \
+_Pragma("unroll") \
+      for (int i = 0; i < 2; ++i) \
+_Pragma("unroll") \
+        for (int t = 0; t < 2; ++t) \
+          in[0][i][t] = epi8_load<BWD, Q8, CHK_>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g); \
+_Pragma("unroll") \
+      for (int h = 0; h < 4; ++h) { \
+        if (h + 1 < 4) { \
+_Pragma("unroll") \
+          for (int i = 0; i < 2; ++i) \
+_Pragma("unroll") \
+            for (int t = 0; t < 2; ++t) \
+              in[(h + 1) & 1][i][t] = epi8_load<BWD, Q8, CHK_>(a, m0 + wr * 128 + (2 * h + 2 + i) * 16 + ii, \
+                                                     n0 + wc * 64 + 32 * t + 8 * g); \
+        } \
+        asm volatile("" ::"v"(in[h & 1][0][0].x), "v"(in[h & 1][0][1].x), "v"(in[h & 1][1][0].x), \
+                     "v"(in[h & 1][1][1].x)); \
+_Pragma("unroll") \
+        for (int i = 0; i < 2; ++i) \
+_Pragma("unroll") \
+          for (int t = 0; t < 2; ++t) { \
+            if (Q8 && BWD) \
+              epi8_q8<ACT, true>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, g, \
+                                 acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], t ? bias1 : bias0, \
+                                 &in[h & 1][i][t], dtab); \
+            else \
+              epi8<ACT, BWD, true, BWD, CHK_>(a, m0 + wr * 128 + (2 * h + i) * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g, \
+                                        acc[2 * h + i][2 * t], acc[2 * h + i][2 * t + 1], in[h & 1][i][t], \
+                                        t ? bias1 : bias0, dtab); \
+          } \
       }
+#ifndef MMSEQ_EPI_CHECK_ALL
+      if (!(Q8 && BWD) && (ACT == 0 || BWD) && m0 + 256 <= a.M && n0 + 256 <= a.N) {
+        XIN_EPI(false)
+      } else
+#endif
+      {
+        XIN_EPI(true)
+      }
+#undef XIN_EPI
     } else if (Q8) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -628,6 +640,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(GemmArgs a, int tile
                        acc[i][2 * t], acc[i][2 * t + 1], t ? bias1 : bias0);
     } else {
       const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
+#ifndef MMSEQ_EPI_CHECK_ALL  // interior tiles without the per-call bounds branches
+      if (m0 + 256 <= a.M && n0 + 256 <= a.N) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            epi8<ACT, BWD, false, false, false>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                                acc[i][2 * t], acc[i][2 * t + 1], none, t ? bias1 : bias0);
+      } else
+#endif
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -994,6 +1016,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tile
       }
     } else {
       const EpiIn none = {(u16x8){0, 0, 0, 0, 0, 0, 0, 0}};
+#ifndef MMSEQ_EPI_CHECK_ALL  // interior tiles without the per-call bounds branches
+      if (m0 + 256 <= a.M && n0 + 256 <= a.N) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            epi8<ACT, BWD, false, false, false>(a, m0 + wr * 128 + i * 16 + ii, n0 + wc * 64 + 32 * t + 8 * g,
+                                                acc[i][2 * t], acc[i][2 * t + 1], none, t ? bias1 : bias0);
+      } else
+#endif
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll

@@ -5,14 +5,14 @@
 #   3. its summaries copied into profiles/TAG_* on the box, so that the bench that follows cites
 #      PMC passes of this same tree (bench.py reads the newest profiles/r*_v*_pmc_*.json)
 #   4. the default bench line
-# usage (repo root, on the box): bash tools/evidence.sh r4_v6
+# usage (repo root, on the box): bash tools/evidence.sh r4_v6 [notests]
 # Everything lands in gpurun_out/TAG/ (copy the summaries into profiles/ afterwards).
 set -euo pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 tag=${1:?tag}
 out=gpurun_out/$tag
 mkdir -p "$out"
-bash tools/gpu_run.sh "$tag" tests smoke
+[ "${2:-}" = notests ] || bash tools/gpu_run.sh "$tag" tests smoke
 bash tools/profile_round.sh "$tag"
 p=gpurun_out/prof_$tag
 cp "$p/kernel_stats.csv" "profiles/${tag}_kernel_stats.csv"
