@@ -12,6 +12,10 @@ this?", independently of the HIP kernels:
   prob     attention probabilities rounded before the P.V product (flash attention's bf16 P)
   stream   the residual stream: the ViT's x after every residual add, the BERT layers' pre-LN
            sums and LayerNorm outputs, the embedding / visn_fc / ln_pre outputs
+  mx       (not in ALL) the four GEMMs of every encoder layer (QKV, attention output, FC1, FC2) take
+           both operands through OCP MX-fp8 quantisation — e4m3 elements, one E8M0 power-of-two
+           scale 2^(floor(log2 amax) - 8) per 32 K-elements — after the bf16 rounding, as
+           kernels.fp8_forward() does (fp32 accumulation of the dequantised values)
 
 ALL = every site is where the product's bf16 mode rounds (kernels.py / the csrc epilogues).
 Follows oracle vit_forward / bert_layer / lxrt_forward (clip/model.py:242-305,
@@ -31,6 +35,20 @@ def _r(t):
     return t.to(torch.bfloat16).float()
 
 
+def mx_fake_quant(t):
+    """t [..., K] -> its MX-fp8 value (dequantised, fp32): per 32 consecutive K-elements the shared
+    exponent e = floor(log2 amax) - 8 (E8M0, clamped to [-127, 127]; all-zero blocks -> 2^-127),
+    elements t / 2^e clamped to +-448 and rounded to float8_e4m3fn (csrc/fp8.hip mmseq_quant_mxfp8)."""
+    shp = t.shape
+    b = t.float().reshape(-1, shp[-1] // 32, 32)
+    amax = b.abs().amax(-1, keepdim=True)
+    e = torch.where(amax > 0, ((amax.view(torch.int32) >> 23) & 0xFF).float() - 127,
+                    torch.full_like(amax, -127.0))
+    e = torch.clamp(e - 8, -127, 127)
+    s = torch.where(amax > 0, torch.exp2(e), torch.ones_like(e))
+    return (torch.clamp(b / s, -448, 448).to(torch.float8_e4m3fn).float() * s).reshape(shp)
+
+
 class Emu:
     def __init__(self, p, sites):
         self.p = p
@@ -47,8 +65,17 @@ class Emu:
             self._w[name] = _r(self.p[name])
         return self._w[name]
 
-    def lin(self, x, name, bias=True):
-        y = self.rnd("operand", x) @ self.w(name + ".weight").t()
+    def mm(self, x, wkey, mx=False):
+        """x @ W^T with the operand / weight rounding (and MX-fp8 quantisation for the layer GEMMs)"""
+        x, w = self.rnd("operand", x), self.w(wkey)
+        if mx and "mx" in self.s:
+            if ("mx", wkey) not in self._w:
+                self._w[("mx", wkey)] = mx_fake_quant(w)
+            x, w = mx_fake_quant(x), self._w[("mx", wkey)]
+        return x @ w.t()
+
+    def lin(self, x, name, bias=True, mx=False):
+        y = self.mm(x, name + ".weight", mx)
         if bias and (name + ".bias") in self.p:
             y = y + self.p[name + ".bias"]
         return y
@@ -86,24 +113,24 @@ class Emu:
         for i in range(nl):
             b = f"{V}transformer.resblocks.{i}."
             h = self.rnd("output", self.ln(x, b + "ln_1", 1e-5))
-            qkv = self.rnd("operand", h) @ self.w(b + "attn.in_proj_weight").t() + p[b + "attn.in_proj_bias"]
+            qkv = self.mm(h, b + "attn.in_proj_weight", True) + p[b + "attn.in_proj_bias"]
             q, k, v = qkv.split(W, -1)
-            x = self.rnd("stream", x + self.lin(self.mha(q, k, v, heads), b + "attn.out_proj"))
+            x = self.rnd("stream", x + self.lin(self.mha(q, k, v, heads), b + "attn.out_proj", mx=True))
             h = self.rnd("output", self.ln(x, b + "ln_2", 1e-5))
-            f = self.rnd("output", O.quick_gelu(self.lin(h, b + "mlp.c_fc")))
-            x = self.rnd("stream", x + self.lin(f, b + "mlp.c_proj"))
+            f = self.rnd("output", O.quick_gelu(self.lin(h, b + "mlp.c_fc", mx=True)))
+            x = self.rnd("stream", x + self.lin(f, b + "mlp.c_proj", mx=True))
         return self.rnd("output", self.rnd("operand", x) @ self.w(V + "proj"))
 
     def bert_layer(self, i, x, key_bias, heads):
         b = f"bert.encoder.layer.{i}."
-        q = self.lin(x, b + "attention.self.query")
-        k = self.lin(x, b + "attention.self.key")
-        v = self.lin(x, b + "attention.self.value")
+        q = self.lin(x, b + "attention.self.query", mx=True)
+        k = self.lin(x, b + "attention.self.key", mx=True)
+        v = self.lin(x, b + "attention.self.value", mx=True)
         a = self.mha(q, k, v, heads, key_bias)
-        s = self.rnd("stream", self.lin(a, b + "attention.output.dense") + x)
+        s = self.rnd("stream", self.lin(a, b + "attention.output.dense", mx=True) + x)
         h = self.rnd("stream", self.ln(s, b + "attention.output.LayerNorm", 1e-12))
-        f = self.rnd("output", O.gelu_erf(self.lin(h, b + "intermediate.dense")))
-        s = self.rnd("stream", self.lin(f, b + "output.dense") + h)
+        f = self.rnd("output", O.gelu_erf(self.lin(h, b + "intermediate.dense", mx=True)))
+        s = self.rnd("stream", self.lin(f, b + "output.dense", mx=True) + h)
         return self.rnd("stream", self.ln(s, b + "output.LayerNorm", 1e-12))
 
     def lxrt(self, ids, mask, tt, images, heads, vit_heads):

@@ -116,3 +116,17 @@ def test_bf16_emulation_without_rounding_is_the_oracle():
         assert torch.equal(ref[k], same[k]), k
     drift = float((r16["lang"] - ref["lang"]).norm() / ref["lang"].norm())
     assert 1e-3 < drift < 2e-2, drift
+
+
+def test_mx_fake_quant_matches_the_quantiser_restatement():
+    """The emulation's MX-fp8 site (tests/bf16_emulation.mx_fake_quant) = dequant(ref_quant(x)) of
+    tests/test_fp8_gpu.py, the restatement the HIP quantiser is bit-exact against (zero blocks,
+    saturating blocks and 10^-6..10^4 magnitudes included)."""
+    import bf16_emulation as E
+    from test_fp8_gpu import dequant, ref_quant
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(37, 256, generator=g)
+    x = x * torch.pow(10.0, torch.randint(-6, 5, (37, 8, 1), generator=g).float()).repeat_interleave(32, -1).view(37, 256)
+    x[0, :32] = 0
+    x = x.bfloat16().float()
+    assert torch.equal(E.mx_fake_quant(x), dequant(*ref_quant(x)))
