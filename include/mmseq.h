@@ -147,6 +147,25 @@ mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv, int64_t ld
                             int64_t ld_dout, const float* lse, float* delta, void* dqkv,
                             int64_t ld_dqkv, mmseq_dtype dtype, const mmseq_dropout* drop,
                             const uint64_t* keep_bits, int variant, mmseq_stream stream);
+/* attn_fwd_rows / attn_bwd_rows: the bf16 fast kernels (variant 1) for the queries 0 .. Tq-1 of
+ *  every sequence against all T keys (1 <= Tq <= T): the last joint layer of the BERSON encoder,
+ *  whose visual rows' outputs _split_with_none discards (lxrt/modeling.py:611-618,
+ *  berson/modeling_bert.py:1289-1290). out / dout hold Tq rows per sequence (row p*Tq + t); lse,
+ *  delta and keep_bits keep the [P][heads][T] layout (rows < Tq written; the dropout index is
+ *  mmseq_attn_fwd's); dqkv is the full [P*T] layout with dQ = 0 on rows >= Tq (dK / dV over every
+ *  key row). Rows < Tq are bit-identical to mmseq_attn_fwd / _bwd with the other rows' dO = 0. */
+mmseq_status mmseq_attn_fwd_rows(int P, int T, int Tq, int heads, const void* qkv, int64_t ld_qkv,
+                                 int64_t q_off, int64_t k_off, int64_t v_off,
+                                 const float* key_bias, float scale, void* out, int64_t ld_out,
+                                 float* lse, const mmseq_dropout* drop, uint64_t* keep_bits,
+                                 mmseq_stream stream);
+mmseq_status mmseq_attn_bwd_rows(int P, int T, int Tq, int heads, const void* qkv, int64_t ld_qkv,
+                                 int64_t q_off, int64_t k_off, int64_t v_off,
+                                 const float* key_bias, float scale, const void* out,
+                                 int64_t ld_out, const void* dout, int64_t ld_dout,
+                                 const float* lse, float* delta, void* dqkv, int64_t ld_dqkv,
+                                 const mmseq_dropout* drop, const uint64_t* keep_bits,
+                                 mmseq_stream stream);
 /* attn_bwd_mxfp8: the bf16 fast backward (variant 1) over the packed Q|K|V layout (q_off 0, k_off
  *  heads*64, v_off 2*heads*64) that also writes dQ|dK|dV in MX-fp8 (q8 [P*T][ldq8] e4m3 + packed
  *  scales of the [P*T][3*heads*64] operand, bit-identical to quantising dqkv; padding-row scales
@@ -227,6 +246,18 @@ mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, mmseq_rows 
                                  float* workspace, mmseq_dtype dtype,
                                  const mmseq_dropout* drop_dy, void* dx_drop,
                                  const mmseq_dropout* drop_dx, mmseq_stream stream);
+/* layernorm_bwd_rows: mmseq_layernorm_bwd with the dropout-masked copy dx_drop in its own row layout
+ *  (mmseq_layernorm_bwd writes it in dx's): the last joint layer on the text rows only
+ *  (mmseq_attn_fwd_rows) writes the residual branch's dx into its rows of the full-size [P*T]
+ *  gradient and the dense branch's masked copy compact (BertSelfOutput, lxrt/modeling.py:431-433). */
+mmseq_status mmseq_layernorm_bwd_rows(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                      const void* x, mmseq_rows xl, const float* mean,
+                                      const float* rstd, const float* gamma, void* dx,
+                                      mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                      float* dgamma, float* dbeta, float* workspace,
+                                      mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                      void* dx_drop, mmseq_rows dx_dropl,
+                                      const mmseq_dropout* drop_dx, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused text embedding + LayerNorm written straight into the joint buffer (BertEmbeddings,

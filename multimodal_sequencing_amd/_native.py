@@ -68,6 +68,13 @@ _SIGS = {
                                                            _vp, ctypes.c_float, _vp, _c_i64, _vp,
                                                            ctypes.c_int, _dp, _vp, ctypes.c_int,
                                                            _vp]),
+    "mmseq_attn_fwd_rows": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
+                                                                _vp, ctypes.c_float, _vp, _c_i64, _vp,
+                                                                _dp, _vp, _vp]),
+    "mmseq_attn_bwd_rows": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
+                                                                _vp, ctypes.c_float, _vp, _c_i64, _vp,
+                                                                _c_i64, _vp, _vp, _vp, _c_i64, _dp,
+                                                                _vp, _vp]),
     "mmseq_attn_fwd_mxfp8": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _c_i64, _c_i64, _c_i64,
                                                            _vp, ctypes.c_float, _vp, _vp, _c_i64,
                                                            _vp, _vp]),
@@ -99,6 +106,9 @@ _SIGS = {
     "mmseq_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
                                            _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
                                            ctypes.c_int, _dp, _vp, _dp, _vp]),
+    "mmseq_layernorm_bwd_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
+                                                _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
+                                                ctypes.c_int, _dp, _vp, Rows, _dp, _vp]),
     "mmseq_layernorm_bwd_mxfp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows,
                                                  _vp, _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
                                                  _dp, _vp, _dp, _vp, _c_i64, _vp, _vp]),
@@ -312,6 +322,27 @@ def attn_bwd(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out
            "mmseq_attn_bwd")
 
 
+def attn_fwd_rows(P, T, Tq, heads, qkv, key_bias, scale, out, lse, drop=None, keep_bits=None):
+    """The bf16 forward for queries 0 .. Tq-1 of every sequence (packed Q|K|V qkv [P*T][3H]):
+    out [P*Tq][H], lse [P][heads][T] (rows < Tq), keep bits in mmseq_attn_fwd's layout."""
+    _dev(qkv, out, lse)
+    H = heads * 64
+    _check(lib().mmseq_attn_fwd_rows(P, T, Tq, heads, _p(qkv), 3 * H, 0, H, 2 * H, _p(key_bias), scale,
+                                     _p(out), H, _p(lse), _d(drop), _p(keep_bits), _stream()),
+           "mmseq_attn_fwd_rows")
+
+
+def attn_bwd_rows(P, T, Tq, heads, qkv, key_bias, scale, out, dout, lse, delta, dqkv, drop=None,
+                  keep_bits=None):
+    """Backward of attn_fwd_rows: out / dout [P*Tq][H]; dqkv [P*T][3H] (dQ = 0 on rows >= Tq)."""
+    _dev(qkv, out, dout, dqkv)
+    H = heads * 64
+    _check(lib().mmseq_attn_bwd_rows(P, T, Tq, heads, _p(qkv), 3 * H, 0, H, 2 * H, _p(key_bias), scale,
+                                     _p(out), H, _p(dout), H, _p(lse), _p(delta), _p(dqkv), 3 * H,
+                                     _d(drop), _p(keep_bits), _stream()),
+           "mmseq_attn_bwd_rows")
+
+
 def small_attn_fwd(B, T, heads, d, q, k, v, key_bias, scale, out, probs, drop=None):
     _check(lib().mmseq_small_attn_fwd(B, T, heads, d, _p(q), _p(k), _p(v), _p(key_bias), scale,
                                       _p(out), _p(probs), _d(drop), _stream()),
@@ -345,9 +376,17 @@ def layernorm_fwd_mxfp8(nrows, cols, x, gamma, beta, eps, y=None, mean=None, rst
 
 
 def layernorm_bwd(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl, dgamma,
-                  dbeta, drop_dy=None, dx_drop=None, drop_dx=None):
+                  dbeta, drop_dy=None, dx_drop=None, drop_dx=None, dx_drop_rows=None):
+    """dx_drop_rows: the row layout of dx_drop (mmseq_layernorm_bwd_rows); default dx's."""
     ws = torch.empty(lib().mmseq_layernorm_bwd_workspace(nrows, cols), dtype=torch.float32,
                      device=x.device)
+    if dx_drop_rows is not None:
+        _check(lib().mmseq_layernorm_bwd_rows(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
+                                              _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
+                                              _p(dbeta), _p(ws), dt(x), _d(drop_dy), _p(dx_drop),
+                                              dx_drop_rows, _d(drop_dx), _stream()),
+               "mmseq_layernorm_bwd_rows")
+        return
     _check(lib().mmseq_layernorm_bwd(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
                                      _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
                                      _p(dbeta), _p(ws), dt(x), _d(drop_dy), _p(dx_drop),

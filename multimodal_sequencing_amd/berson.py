@@ -178,7 +178,7 @@ class BertForOrdering(nn.Module):
                                            attention_mask.reshape(P, Lt),
                                            token_type_ids.reshape(P, Lt),
                                            images if not self.bert.text_part else None,
-                                           pairs_list, drops=D)
+                                           pairs_list, drops=D, text_rows=True)
         top = joint[:, :Lt].float()  # lang_feats (:1289), fp32 for the head
         cls_pooled = top[:, 0]  # :1290
         # ---- HierarchicalAttention (:686-817) -------------------------------------------

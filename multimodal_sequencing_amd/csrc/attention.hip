@@ -46,6 +46,9 @@ struct AttnArgs {
   // tail fold (bf16 dK/dV kernel): when 1 <= T % 128 <= 16 the last 128-row block of each (pair,
   // head) also owns rows tail0 .. T-1 (tail0 = 128 * (T / 128)); 0 = no fold. nxq = row blocks.
   int tail0, nxq;
+  // query rows per pair (bf16 fast kernels; the other kernels take Tq == T): queries 0 .. Tq-1 of
+  // every pair against all T keys; O / dO hold Tq rows per pair (row p * Tq + q)
+  int Tq;
   // bf16 forward, Q8: the output in MX-fp8 (fp8.hip layout) instead of bf16: e4m3 [P*T][ldq8] +
   // packed scales for (P*T, heads*64) columns
   uint8_t* q8; int64_t ldq8; uint8_t* q8s;
@@ -690,11 +693,11 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
   const int T = a.T;
-  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const BlkIdx bi = attn_block((a.Tq + 127) >> 7, a.heads);
   const int h = bi.h, p = bi.p;
   const int nkt = (T + 63) >> 6;
   const int qw = bi.x * 128 + wave * 32;
-  const bool active = qw < T;
+  const bool active = qw < a.Tq;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
   const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
@@ -918,11 +921,11 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
   for (int grp = 0; grp < 2; ++grp) {
     const float lt = lsum[grp][0];
     const int q = qw + grp * 16 + i;
-    if (q < T) {
+    if (q < a.Tq) {
       const float inv = (DROP ? a.drop.scale : 1.0f) / lt;
       if (Q8) {  // MX-fp8 of the bf16-rounded output (bit-identical to bf16 out + mmseq_quant_mxfp8):
                  // block b of the head's 64 columns = d 2b, 2b+1 of the four lanes g of query i
-        const int64_t row = (int64_t)p * T + q;
+        const int64_t row = (int64_t)p * a.Tq + q;
         const int KB = a.heads * 2;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
@@ -959,7 +962,7 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
           }
         }
       } else {
-        unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * T + q) * a.ld_out +
+        unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * a.Tq + q) * a.ld_out +
                              h * 64 + 4 * g;
 #pragma unroll
         for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(op + d * 16, o[grp][d] * inv);
@@ -1278,11 +1281,11 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
   const int T = a.T;
-  const BlkIdx bi = attn_block((T + 127) >> 7, a.heads);
+  const BlkIdx bi = attn_block((a.Tq + 127) >> 7, a.heads);
   const int h = bi.h, p = bi.p;
   const int nkt = (T + 63) >> 6;
   const int qw = bi.x * 128 + wave * 32;
-  const bool active = qw < T;
+  const bool active = qw < a.Tq;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
   const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
@@ -1310,17 +1313,12 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
   float kbv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) kbv[j] = buf_f32(rkb, tid + 256 * j);
-  const unsigned short* Qb = reinterpret_cast<const unsigned short*>(a.qkv) + (int64_t)p * T * ld +
-                             a.q_off + h * 64;
-  const unsigned short* dOb = reinterpret_cast<const unsigned short*>(a.dout) +
-                              (int64_t)p * T * a.ld_dout + h * 64;
-  const unsigned short* Ob = reinterpret_cast<const unsigned short*>(a.out) +
-                             (int64_t)p * T * a.ld_out + h * 64;
   bf16x8_t qf[2][2], of[2][2], ovf[2][2];
   float L2[2], Dd[2];
   const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
-  const rsrc_t rdo = head_rsrc(a.dout, (int64_t)p * T, a.ld_dout, h * 64, T);
-  const rsrc_t rout = head_rsrc(a.out, (int64_t)p * T, a.ld_out, h * 64, T);
+  // O / dO: Tq rows per pair (rows >= Tq read as zero: their dS and dQ are zero)
+  const rsrc_t rdo = head_rsrc(a.dout, (int64_t)p * a.Tq, a.ld_dout, h * 64, a.Tq);
+  const rsrc_t rout = head_rsrc(a.out, (int64_t)p * a.Tq, a.ld_out, h * 64, a.Tq);
   const rsrc_t rlse = make_rsrc(a.lse + ((int64_t)p * a.heads + h) * T, (int64_t)T * 4);
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
@@ -1353,7 +1351,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     dot += __shfl_xor(dot, 32, 64);
     Dd[grp] = dot;
     const int64_t ri = ((int64_t)p * a.heads + h) * T + q;
-    L2[grp] = q < T ? L2[grp] * LOG2E : 1e30f;
+    L2[grp] = q < a.Tq ? L2[grp] * LOG2E : 1e30f;
     if (q < T && g == 0) a.delta[ri] = dot;
     settle(qf[grp][0]);
     settle(qf[grp][1]);
@@ -1461,13 +1459,21 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
   }
 }
 
+// rows >= Tq have no query (a Tq < T backward, mmseq_attn_bwd_rows): their dQ slice of head h is
+// zero; the dK / dV kernel, which owns every key row, writes it
+__device__ __forceinline__ void zero_dq(const AttnArgs& a, unsigned short* row, int h, int g) {
+  unsigned short* dqp = row + a.q_off + h * 64 + 4 * g;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(dqp + d * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
+}
+
 // ---- backward: dK, dV (per 128-key block, queries swept; key on the MFMA lane) ----------------
 template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
 __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (Q, dO) + lse, D
-  const int T = a.T;
-  const int nqt = (T + 63) >> 6;
+  const int T = a.T, Tq = a.Tq;
+  const int nqt = (Tq + 63) >> 6;  // the queries swept: rows < Tq (the others have dO = 0)
   float* sL = reinterpret_cast<float*>(smem + 4 * IMG);
   float* sD = sL + nqt * 64;
   // keep-bit words of the q-tile for this block's two key tiles: [2 buffers][64 q][4 dwords]
@@ -1490,7 +1496,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   const bool tailb = DMODE != 1 && a.tail0 > 0 && bi.x == a.nxq - 1;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
-  const rsrc_t ro = head_rsrc(a.dout, (int64_t)p * T, a.ld_dout, h * 64, T);
+  const rsrc_t ro = head_rsrc(a.dout, (int64_t)p * Tq, a.ld_dout, h * 64, Tq);
   const uint32_t loffq = dma_lane_off(lane, ld), loffo = dma_lane_off(lane, a.ld_dout);
   const int64_t bh = (int64_t)p * a.heads + h;
   const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + bh * T * a.nkt2, (int64_t)T * a.nkt2 * 8)
@@ -1554,13 +1560,13 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   for (int j = 0; j < 4; ++j) {
     const int q = tid + 256 * j;
     if (q < nqt * 64) {
-      sL[q] = q < T ? lv[j] * LOG2E : 1e30f;  // exp2(x - 1e30) = 0 for padded queries
-      sD[q] = q < T ? dlv[j] : 0.f;
+      sL[q] = q < Tq ? lv[j] * LOG2E : 1e30f;  // exp2(x - 1e30) = 0 for padded queries
+      sD[q] = q < Tq ? dlv[j] : 0.f;
     }
   }
   for (int q = tid + 1024; q < nqt * 64; q += 256) {
-    sL[q] = q < T ? buf_f32(rlse, q) * LOG2E : 1e30f;
-    sD[q] = q < T ? buf_f32(rdel, q) : 0.f;
+    sL[q] = q < Tq ? buf_f32(rlse, q) * LOG2E : 1e30f;
+    sD[q] = q < Tq ? buf_f32(rdel, q) : 0.f;
   }
   if (tailb && wave == 0) {
 #pragma unroll
@@ -1771,6 +1777,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
           q8_head_row(a, (int64_t)p * T + key, (int)a.k_off + h * 64, dkt, a.scale, g);
           q8_head_row(a, (int64_t)p * T + key, (int)a.v_off + h * 64, dvt, 1.f, g);
         }
+        if (key >= Tq) zero_dq(a, row, h, g);
       }
     }
   }
@@ -1791,6 +1798,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
         q8_head_row(a, (int64_t)p * T + key, (int)a.k_off + h * 64, dk[grp], a.scale, g);
         q8_head_row(a, (int64_t)p * T + key, (int)a.v_off + h * 64, dv[grp], 1.f, g);
       }
+      if (key >= Tq) zero_dq(a, row, h, g);
     }
   }
 }
@@ -1826,18 +1834,19 @@ mmseq_status check_common(int P, int T, int heads, const void* qkv, int64_t ld, 
 
 }  // namespace
 
-extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
-                                       int64_t q_off, int64_t k_off, int64_t v_off,
-                                       const float* key_bias, float scale, void* out,
-                                       int64_t ld_out, float* lse, mmseq_dtype dtype,
-                                       const mmseq_dropout* drop, uint64_t* keep_bits,
-                                       int variant, mmseq_stream stream) {
+static mmseq_status attn_fwd_impl(int P, int T, int Tq, int heads, const void* qkv, int64_t ld_qkv,
+                                  int64_t q_off, int64_t k_off, int64_t v_off,
+                                  const float* key_bias, float scale, void* out, int64_t ld_out,
+                                  float* lse, mmseq_dtype dtype, const mmseq_dropout* drop,
+                                  uint64_t* keep_bits, int variant, mmseq_stream stream) {
   mmseq_status st = check_common(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, dtype);
   if (st) return st;
   MMSEQ_REQUIRE(out && lse && ld_out >= heads * 64, "attn_fwd: bad out/lse");
+  MMSEQ_REQUIRE(Tq >= 1 && Tq <= T && (Tq == T || (dtype == MMSEQ_BF16 && variant == 1)),
+                "attn_fwd: Tq=%d (1 <= Tq <= T; Tq < T needs the bf16 variant-1 kernels)", Tq);
   if (P == 0) return MMSEQ_OK;
   AttnArgs a = {};
-  a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
+  a.P = P; a.T = T; a.Tq = Tq; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
   a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
   a.o_w = out; a.ld_out = ld_out; a.lse = lse;
   a.drop = make_drop(drop);
@@ -1862,7 +1871,7 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
       hipLaunchKernelGGL((attn_fwd32_kernel<0, false>), gq, dim3(128), lds, s, a);
   } else if (dtype == MMSEQ_BF16 && variant) {
     MMSEQ_REQUIRE(aligned16(out) && ld_out % 8 == 0, "attn_fwd: out must be 16-byte aligned rows");
-    const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
+    const dim3 gq((unsigned)(((Tq + 127) / 128) * heads * P));
     size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * (64 + 1) * 4;
 #ifdef MMSEQ_ATTN_FWD_LDS_PAD  // occupancy experiments: pad the workgroup's LDS
     lds += MMSEQ_ATTN_FWD_LDS_PAD;
@@ -1886,7 +1895,27 @@ extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv,
   return mmseq_check_launch("attn_fwd");
 }
 
-static mmseq_status attn_bwd_impl(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+extern "C" mmseq_status mmseq_attn_fwd(int P, int T, int heads, const void* qkv, int64_t ld_qkv,
+                                       int64_t q_off, int64_t k_off, int64_t v_off,
+                                       const float* key_bias, float scale, void* out,
+                                       int64_t ld_out, float* lse, mmseq_dtype dtype,
+                                       const mmseq_dropout* drop, uint64_t* keep_bits,
+                                       int variant, mmseq_stream stream) {
+  return attn_fwd_impl(P, T, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,
+                       lse, dtype, drop, keep_bits, variant, stream);
+}
+
+extern "C" mmseq_status mmseq_attn_fwd_rows(int P, int T, int Tq, int heads, const void* qkv,
+                                            int64_t ld_qkv, int64_t q_off, int64_t k_off,
+                                            int64_t v_off, const float* key_bias, float scale,
+                                            void* out, int64_t ld_out, float* lse,
+                                            const mmseq_dropout* drop, uint64_t* keep_bits,
+                                            mmseq_stream stream) {
+  return attn_fwd_impl(P, T, Tq, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out,
+                       ld_out, lse, MMSEQ_BF16, drop, keep_bits, 1, stream);
+}
+
+static mmseq_status attn_bwd_impl(int P, int T, int Tq, int heads, const void* qkv, int64_t ld_qkv,
                                   int64_t q_off, int64_t k_off, int64_t v_off,
                                   const float* key_bias, float scale, const void* out,
                                   int64_t ld_out, const void* dout, int64_t ld_dout,
@@ -1900,9 +1929,11 @@ static mmseq_status attn_bwd_impl(int P, int T, int heads, const void* qkv, int6
   MMSEQ_REQUIRE(out && dout && lse && delta && dqkv, "attn_bwd: null buffer");
   MMSEQ_REQUIRE(aligned16(dout) && ld_dout % ve == 0 && ld_dqkv >= ld_qkv - 0 && ld_dqkv % 1 == 0,
                 "attn_bwd: dout alignment");
+  MMSEQ_REQUIRE(Tq >= 1 && Tq <= T && (Tq == T || (dtype == MMSEQ_BF16 && variant && !q8)),
+                "attn_bwd: Tq=%d (1 <= Tq <= T; Tq < T needs the bf16 fast kernels, no MX-fp8 copy)", Tq);
   if (P == 0) return MMSEQ_OK;
   AttnArgs a = {};
-  a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
+  a.P = P; a.T = T; a.Tq = Tq; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
   a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
   a.out = out; a.ld_out = ld_out; a.dout = dout; a.ld_dout = ld_dout;
   a.lse = const_cast<float*>(lse); a.delta = delta; a.dqkv = dqkv; a.ld_dqkv = ld_dqkv;
@@ -1930,7 +1961,7 @@ static mmseq_status attn_bwd_impl(int P, int T, int heads, const void* qkv, int6
     // the dQ kernel does not fold: its tail state took it from three to two waves per SIMD
     // (148 -> 236 VGPRs), slower at T = 513 and 393 than the extra block it saves
     tail_fold(a, 0);
-    const dim3 gdq((unsigned)(a.nxq * heads * P)), gdk((unsigned)(ak.nxq * heads * P));
+    const dim3 gdq((unsigned)(((Tq + 127) / 128) * heads * P)), gdk((unsigned)(ak.nxq * heads * P));
     if (dmode == 2) {
       hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gdq, dim3(256), lds, s, a);
       hipLaunchKernelGGL(attn_dkdv_bf16_kernel<2>, gdk, dim3(256), ldsk, s, ak);
@@ -1961,8 +1992,20 @@ extern "C" mmseq_status mmseq_attn_bwd(int P, int T, int heads, const void* qkv,
                                        int64_t ld_dqkv, mmseq_dtype dtype,
                                        const mmseq_dropout* drop, const uint64_t* keep_bits,
                                        int variant, mmseq_stream stream) {
-  return attn_bwd_impl(P, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,
+  return attn_bwd_impl(P, T, T, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,
                        dout, ld_dout, lse, delta, dqkv, ld_dqkv, dtype, drop, keep_bits, variant,
+                       nullptr, 0, nullptr, stream);
+}
+
+extern "C" mmseq_status mmseq_attn_bwd_rows(int P, int T, int Tq, int heads, const void* qkv,
+                                            int64_t ld_qkv, int64_t q_off, int64_t k_off,
+                                            int64_t v_off, const float* key_bias, float scale,
+                                            const void* out, int64_t ld_out, const void* dout,
+                                            int64_t ld_dout, const float* lse, float* delta,
+                                            void* dqkv, int64_t ld_dqkv, const mmseq_dropout* drop,
+                                            const uint64_t* keep_bits, mmseq_stream stream) {
+  return attn_bwd_impl(P, T, Tq, heads, qkv, ld_qkv, q_off, k_off, v_off, key_bias, scale, out, ld_out,
+                       dout, ld_dout, lse, delta, dqkv, ld_dqkv, MMSEQ_BF16, drop, keep_bits, 1,
                        nullptr, 0, nullptr, stream);
 }
 
@@ -1977,7 +2020,7 @@ extern "C" mmseq_status mmseq_attn_bwd_mxfp8(int P, int T, int heads, const void
   const int64_t H = (int64_t)heads * 64;
   MMSEQ_REQUIRE(q8 && q8_scales && ldq8 >= 3 * H && ldq8 % 16 == 0 && ((uintptr_t)q8 & 15) == 0,
                 "attn_bwd_mxfp8: q8 / ldq8");
-  return attn_bwd_impl(P, T, heads, qkv, ld_qkv, 0, H, 2 * H, key_bias, scale, out, ld_out, dout,
+  return attn_bwd_impl(P, T, T, heads, qkv, ld_qkv, 0, H, 2 * H, key_bias, scale, out, ld_out, dout,
                        ld_dout, lse, delta, dqkv, ld_dqkv, MMSEQ_BF16, drop, keep_bits, 1, q8, ldq8,
                        q8_scales, stream);
 }
@@ -2003,7 +2046,7 @@ extern "C" mmseq_status mmseq_attn_fwd_mxfp8_dual(int P, int T, int heads, const
                 "attn_fwd_mxfp8: bf16 out must be 8-byte aligned rows");
   if (P == 0) return MMSEQ_OK;
   AttnArgs a = {};
-  a.P = P; a.T = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
+  a.P = P; a.T = T; a.Tq = T; a.heads = heads; a.qkv = qkv; a.ld_qkv = ld_qkv;
   a.q_off = q_off; a.k_off = k_off; a.v_off = v_off; a.key_bias = key_bias; a.scale = scale;
   a.lse = lse; a.drop = make_drop(drop);
   a.o_w = out; a.ld_out = ld_out;

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
                                                      T* __restrict__ dx, mmseq_rows dxl,
                                                      const T* __restrict__ dres, mmseq_rows dresl,
                                                      float* __restrict__ ws, Drop din,
-                                                     T* __restrict__ dxd, Drop dout) {
+                                                     T* __restrict__ dxd, mmseq_rows dxdl, Drop dout) {
   __shared__ float red[4][2][256 * MAXJ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4 pg[MAXJ], pb[MAXJ], gm[MAXJ];
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
         drop_mul4(dout, (uint64_t)r * cols + c, dm);
 #pragma unroll
         for (int e = 0; e < 4; ++e) od[e] = o[e] * dm[e];
-        st4<T, VEC>(dxd + row_off(dxl, r), c, cols, od);
+        st4<T, VEC>(dxd + row_off(dxdl, r), c, cols, od);
       }
       if (drr) {
         f32x4 dr = ld4<T, VEC>(drr, c, cols);
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const
                                                        us* __restrict__ dx, mmseq_rows dxl,
                                                        const us* __restrict__ dres, mmseq_rows dresl,
                                                        float* __restrict__ ws, Drop din,
-                                                       us* __restrict__ dxd, Drop dout,
+                                                       us* __restrict__ dxd, mmseq_rows dxdl, Drop dout,
                                                        uint8_t* __restrict__ q8 = nullptr,
                                                        int64_t ldq = 0, uint8_t* __restrict__ q8s = nullptr) {
   __shared__ float red[4][2][NJ * 256];
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const
 #pragma unroll
         for (int e = 0; e < 8; ++e) od[e] = o[e] * dm2[e];
         qsrc = pack8(od);
-        *reinterpret_cast<u16x8*>(dxd + row_off(dxl, r) + c) = qsrc;
+        *reinterpret_cast<u16x8*>(dxd + row_off(dxdl, r) + c) = qsrc;
       }
       if (drr) {
         float t[8];
@@ -603,8 +603,8 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
                                        mmseq_rows dxl, const void* dres, mmseq_rows dresl,
                                        float* dgamma, float* dbeta, float* workspace,
                                        mmseq_dtype dtype, const mmseq_dropout* drop_dy,
-                                       void* dx_drop, const mmseq_dropout* drop_dx, void* q,
-                                       int64_t ldq, void* q_scales, mmseq_stream stream) {
+                                       void* dx_drop, mmseq_rows dxdl, const mmseq_dropout* drop_dx,
+                                       void* q, int64_t ldq, void* q_scales, mmseq_stream stream) {
   MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 2048, "layernorm_bwd: cols must be in (0, 2048]");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "layernorm_bwd: null buffer");
   if (rows == 0) return MMSEQ_OK;
@@ -614,19 +614,19 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
   const int esz = dtype == MMSEQ_BF16 ? 2 : 4;
   const bool vec = cols % 4 == 0 && rows_vec(dy, dyl, esz) && rows_vec(x, xl, esz) &&
                    rows_vec(dx, dxl, esz) && (!dres || rows_vec(dres, dresl, esz)) &&
-                   (!dx_drop || ((uintptr_t)dx_drop % (4 * esz)) == 0);
+                   (!dx_drop || rows_vec(dx_drop, dxdl, esz));
   const Drop din = make_drop(drop_dy), dout = make_drop(drop_dx);
   if (dtype == MMSEQ_BF16 && cols % 256 == 0 && cols <= 1024 && rows_vec16(dy, dyl) && rows_vec16(x, xl) &&
       rows_vec16(dx, dxl) && (!dres || rows_vec16(dres, dresl)) &&
-      (!dx_drop || ((uintptr_t)dx_drop % 16) == 0) && ((uintptr_t)gamma % 16) == 0) {
+      (!dx_drop || rows_vec16(dx_drop, dxdl)) && ((uintptr_t)gamma % 16) == 0) {
     const int nb16 = (rows + RPB16 - 1) / RPB16;
     const bool di = din.thr != 0, dd = dx_drop != nullptr;
 #define LNB16K(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B>), dim3(nb16), dim3(256), 0, s, rows, \
                     cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,         \
-                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dout, nullptr, 0, nullptr)
+                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, nullptr, 0, nullptr)
 #define LNB16Q(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B, true>), dim3(nb16), dim3(256), 0, s, \
                     rows, cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,   \
-                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dout, (uint8_t*)q, ldq,       \
+                    (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, (uint8_t*)q, ldq, \
                     (uint8_t*)q_scales)
 #define LNB16(NJ)                                           \
   if (q) {                                                  \
@@ -654,7 +654,7 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
 #define LNBJ(T, V, J)                                                                             \
   hipLaunchKernelGGL((ln_bwd_kernel<T, V, J>), dim3(nb), dim3(256), 0, s, rows, cols, (const T*)dy, \
                      dyl, (const T*)x, xl, mean, rstd, gamma, (T*)dx, dxl, (const T*)dres, dresl,   \
-                     workspace, din, (T*)dx_drop, dout)
+                     workspace, din, (T*)dx_drop, dxdl, dout)
 #define LNB(T, V) \
   if (cols <= 1024) { LNBJ(T, V, 4); } else { LNBJ(T, V, 8); }
   if (dtype == MMSEQ_F32) {
@@ -679,8 +679,22 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
                                             void* dx_drop, const mmseq_dropout* drop_dx,
                                             mmseq_stream stream) {
   return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
-                            dgamma, dbeta, workspace, dtype, drop_dy, dx_drop, drop_dx, nullptr, 0,
-                            nullptr, stream);
+                            dgamma, dbeta, workspace, dtype, drop_dy, dx_drop, dxl, drop_dx, nullptr,
+                            0, nullptr, stream);
+}
+
+extern "C" mmseq_status mmseq_layernorm_bwd_rows(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                                 const void* x, mmseq_rows xl, const float* mean,
+                                                 const float* rstd, const float* gamma, void* dx,
+                                                 mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                                 float* dgamma, float* dbeta, float* workspace,
+                                                 mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                                 void* dx_drop, mmseq_rows dx_dropl,
+                                                 const mmseq_dropout* drop_dx, mmseq_stream stream) {
+  MMSEQ_REQUIRE(dx_drop, "layernorm_bwd_rows: dx_drop is required");
+  return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
+                            dgamma, dbeta, workspace, dtype, drop_dy, dx_drop, dx_dropl, drop_dx,
+                            nullptr, 0, nullptr, stream);
 }
 
 extern "C" mmseq_status mmseq_layernorm_bwd_mxfp8(int rows, int cols, const void* dy, mmseq_rows dyl,
@@ -694,8 +708,8 @@ extern "C" mmseq_status mmseq_layernorm_bwd_mxfp8(int rows, int cols, const void
   MMSEQ_REQUIRE(q && q_scales && ldq >= cols && ldq % 16 == 0 && ((uintptr_t)q & 15) == 0,
                 "layernorm_bwd_mxfp8: q / ldq");
   return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
-                            dgamma, dbeta, workspace, MMSEQ_BF16, drop_dy, dx_drop, drop_dx, q, ldq,
-                            q_scales, stream);
+                            dgamma, dbeta, workspace, MMSEQ_BF16, drop_dy, dx_drop, dxl, drop_dx, q,
+                            ldq, q_scales, stream);
 }
 
 extern "C" mmseq_status mmseq_layernorm_fwd_mxfp8(int rows, int cols, const void* x, mmseq_rows xl,

@@ -10,6 +10,7 @@ each Function takes an `anchor` tensor that requires grad so the graph is record
 None for it.
 """
 import math
+import os
 
 import torch
 
@@ -223,20 +224,38 @@ class LayerRefs:
         return out
 
 
+# the last joint layer on the text rows only (BertLayerFn Tq); off (or MMSEQ_ROWS=0 in the
+# environment, for A/B runs): every layer over all T rows
+ROWS = {"on": os.environ.get("MMSEQ_ROWS", "1") != "0"}
+
+
 # ================================================================================================
 # BERT layer (post-LN), lxrt/modeling.py:496-507 (BertSelfattLayer + BertIntermediate + BertOutput)
 # ================================================================================================
 class BertLayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps, drops=(None, None, None), save=True):
+    def rows_ok(x):
+        """The layer can run on the first Tq rows of every sequence only (forward(..., Tq)): bf16,
+        the variant-1 attention kernels (mmseq_attn_fwd_rows), no MX-fp8 path active."""
+        return ROWS["on"] and x.dtype == torch.bfloat16 and N._sel["attn"] == 1 and not _FP8["on"]
+
+    @staticmethod
+    def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps, drops=(None, None, None), save=True,
+                Tq=None):
         """drops = (attention probs :419, self-output dense :437, output dense :491); save=False
         (the caller runs under no_grad) skips the stores only the backward reads (GELU
-        pre-activation)."""
+        pre-activation). Tq (< T, rows_ok): only the first Tq rows of every sequence leave the
+        layer (the last joint layer, whose visual rows _split_with_none discards,
+        lxrt/modeling.py:611-618): QKV over all T rows (the keys and values), everything after
+        the attention on the P * Tq text rows; returns [P * Tq][H]."""
         st = L.store
         H = x.shape[-1]
         d_att, d_o, d_out = drops
         Wqkv = st.packed(L.qkv_w, "w")
         bqkv = st.packed(L.qkv_b, "f32").view(-1)
+        if Tq is not None and Tq < T:
+            return BertLayerFn._forward_rows(ctx, x, key_bias, L, P, T, Tq, heads, eps, drops, save,
+                                             Wqkv, bqkv)
         if save and _f8_train(x, Wqkv, st.w(L.o_w), st.w(L.i_w), st.w(L.out_w)):
             return BertLayerFn._forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv)
         f8 = not save and _f8(x, Wqkv) and d_att is None and d_o is None
@@ -278,6 +297,45 @@ class BertLayerFn(torch.autograd.Function):
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
         ctx.meta = (L, P, T, heads, drops)
         ctx.kbits = kbits
+        return y
+
+    @staticmethod
+    def _forward_rows(ctx, x, key_bias, L, P, T, Tq, heads, eps, drops, save, Wqkv, bqkv):
+        """forward() with Tq < T. Every kept row equals the full-size layer's; in train mode the
+        attention-probability mask too (mmseq_attn_fwd_rows draws it by the full-size index), while
+        the two hidden-dropout sites after the attention (:437, :491) index their masks by the
+        compacted [P * Tq][H] layout: an equally distributed draw, regenerated identically by
+        this layer's backward."""
+        st = L.store
+        H = x.shape[-1]
+        d_att, d_o, d_out = drops
+        qkv = _linear(x, Wqkv, bias=bqkv)
+        lse = torch.empty(P, heads, T, device=x.device)
+        o = torch.empty(P * Tq, H, device=x.device, dtype=x.dtype)
+        kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None and save else None
+        N.attn_fwd_rows(P, T, Tq, heads, qkv, key_bias, 1.0 / math.sqrt(H // heads), o, lse,
+                        drop=d_att, keep_bits=kbits)
+        xt = x.view(P, T, H)[:, :Tq].reshape(P * Tq, H)  # the residual's text rows
+        s1 = _linear(o, st.w(L.o_w), bias=st.f32(L.o_b), resid=xt, drop=d_o)
+        del xt
+        R = P * Tq
+        h1 = torch.empty_like(s1)
+        m1 = torch.empty(R, device=x.device)
+        r1 = torch.empty_like(m1)
+        N.layernorm_fwd(R, H, s1, _rows(H), st.f32(L.ln1_w), st.f32(L.ln1_b), eps, h1, _rows(H), m1, r1)
+        z = torch.empty(R, st.w(L.i_w).shape[0], device=x.device, dtype=x.dtype) if save else None
+        gact = _linear(h1, st.w(L.i_w), bias=st.f32(L.i_b), act=GELU, aux=z)
+        s2 = _linear(gact, st.w(L.out_w), bias=st.f32(L.out_b), resid=h1, drop=d_out)
+        y = torch.empty_like(s1)
+        m2 = torch.empty_like(m1)
+        r2 = torch.empty_like(m1)
+        N.layernorm_fwd(R, H, s2, _rows(H), st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y, _rows(H), m2, r2)
+        if not save:
+            return y
+        ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
+        ctx.meta = (L, P, T, heads, drops)
+        ctx.kbits = kbits
+        ctx.Tq = Tq
         return y
 
     @staticmethod
@@ -349,11 +407,12 @@ class BertLayerFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2 = ctx.saved_tensors
         L, P, T, heads, (d_att, d_o, d_out) = ctx.meta
+        Tq = getattr(ctx, "Tq", T)  # < T: the rows after the attention are the P * Tq text rows
         st = L.store
         st.grad_begin()
         H = x.shape[-1]
         dy = dy.contiguous()
-        R = x.shape[0]
+        R = dy.shape[0]
         # LN backward also emits the dense-branch gradient through the dropout mask (ds2d) while
         # the residual branch keeps the unmasked one (ds2)
         ds2 = torch.empty_like(dy)
@@ -373,16 +432,35 @@ class BertLayerFn(torch.autograd.Function):
         _wgrad(dz, h1, st.g(L.i_w), st.g(L.i_b))
         dh1 = _dgrad8(dz, st, st.wt(L.i_w), resid=ds2, dyq=dzq) if f8 else _dgrad(dz, st.wt(L.i_w), resid=ds2)
         del dz, dzq
-        ds1 = torch.empty_like(dy)
-        ds1d = torch.empty_like(dy) if d_o is not None else ds1
-        ds1q = lnb(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
-                   None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
-                   dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
+        if Tq < T:  # the residual branch's gradient goes straight into its rows of the full-size
+            # [P * T] buffer the QKV dgrad adds in fp32 (zero on the visual rows: bit-identical to
+            # the full-size layer); the dense branch's (masked) copy stays compact
+            ds1 = torch.empty(P * T, H, device=dy.device, dtype=dy.dtype)
+            ds1.view(P, T, H)[:, Tq:].zero_()
+            ds1d = torch.empty_like(dy)
+            N.layernorm_bwd(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1,
+                            N.rows(H, T * H, Tq), None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
+                            dx_drop=ds1d, drop_dx=d_o, dx_drop_rows=_rows(H))
+            ds1q = None
+        else:
+            ds1 = torch.empty_like(dy)
+            ds1d = torch.empty_like(dy) if d_o is not None else ds1
+            ds1q = lnb(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
+                       None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
+                       dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
         _wgrad(ds1d, o, st.g(L.o_w), st.g(L.o_b))
         do = _dgrad8(ds1d, st, st.wt(L.o_w), dyq=ds1q) if f8 else _dgrad(ds1d, st.wt(L.o_w))
         del ds1d
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=x.device)
+        if Tq < T:  # dQ = 0 on the rows past Tq; dK / dV over every key row
+            N.attn_bwd_rows(P, T, Tq, heads, qkv, key_bias, 1.0 / math.sqrt(H // heads), o, do, lse,
+                            delta, dqkv, drop=d_att, keep_bits=ctx.kbits)
+            ctx.kbits = None
+            _wgrad(dqkv, x, st.packed(L.qkv_w, "g"), st.packed(L.qkv_b, "g").view(-1))
+            st.grad_ready(L.span)
+            dx = _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
+            return dx, None, None, None, None, None, None, None, None, None, None
         if f8:  # dQ|dK|dV also in MX-fp8: the QKV dgrad's operand
             dqkvq = N.attn_bwd_mxfp8(P, T, heads, qkv, key_bias, 1.0 / math.sqrt(H // heads), o, do,
                                      lse, delta, dqkv, drop=d_att, keep_bits=ctx.kbits)
@@ -394,7 +472,7 @@ class BertLayerFn(torch.autograd.Function):
         st.grad_ready(L.span)
         dx = _dgrad8(dqkv, st, st.wt(L.qkv_w[0]), resid=ds1, dyq=dqkvq) if f8 else \
             _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
-        return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
 # ================================================================================================

@@ -261,9 +261,12 @@ class LXRTModel(nn.Module):
         return K.VitProjFn.apply(h, self._anchor, self.proj_refs), Tv
 
     def encode_joint(self, input_ids, attention_mask, token_type_ids=None, images=None,
-                     pairs_list=None, drops=None):
+                     pairs_list=None, drops=None, text_rows=False):
         """Run embeddings (+ ViT + visn_fc) and the joint BERT stack.
-        Returns the joint activation [P][T][H] (compute dtype) and Lt."""
+        Returns the joint activation [P][T][H] (compute dtype) and Lt. text_rows=True (the caller
+        keeps only lang_feats, as BertForOrdering.encode, modeling_bert.py:1289-1290): the last
+        layer may run on the text rows only (BertLayerFn Tq, where rows_ok), and the activation
+        returned is then [P][Lt][H] — identical rows, the same dropout masks."""
         st = self.store
         D = drops or self.new_dropouts()
         ph = self.config.hidden_dropout_prob
@@ -285,11 +288,13 @@ class LXRTModel(nn.Module):
                                            (D.site(ph, "emb"), D.site(ph, "visn_fc")))
         heads = self.config.num_attention_heads
         save = torch.is_grad_enabled()
+        nl = len(self.layer_refs)
+        Tq = Lt if text_rows and Tv > 0 and K.BertLayerFn.rows_ok(x) else None
         for i, L in enumerate(self.layer_refs):
             x = K.BertLayerFn.apply(x, key_bias, self._anchor, L, P, T, heads, 1e-12,
                                     (D.site(pa, "att", i), D.site(ph, "att_out", i),
-                                     D.site(ph, "out", i)), save)
-        return x.view(P, T, -1), Lt
+                                     D.site(ph, "out", i)), save, Tq if i == nl - 1 else None)
+        return x.view(P, Tq if Tq and nl else T, -1), Lt
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, visual_feats=None,
                 visual_attention_mask=None, pretraining_objective=None, labels=None,

@@ -425,21 +425,29 @@ def test_config5_fp8_training_forward_tracks_bf16():
     meta, (m16, m8), inputs = _c5_pair()
     m8d = _c5_pair()[1][0]
     losses, grads = {}, {}
-    for name, m in (("bf16", m16), ("fp8", m8), ("fp8_dgrad", m8d)):
-        m.train()
-        opt = FusedAdamW(m.stores(), lr=1e-5, warmup=0, total_steps=10)
-        with K.fp8_forward(name != "bf16", training=True, dgrad=name == "fp8_dgrad"):
-            ls = []
-            for i in range(3):
-                if i == 0:  # the first step's gradients, before the update
-                    m.zero_grad()
-                    m(inputs)[0].backward()
-                    grads[name] = torch.cat([s.grad.clone() for s in m.stores()])
-                    m.zero_grad()
-                ls.append(float(train_step(m, opt, [inputs])))
-            if name != "bf16":
-                assert len(K._FP8["cache"]) >= (32 if name == "fp8_dgrad" else 16)
-        losses[name] = ls
+    # every run over all T rows in its last layer: the bf16 run's text-rows-only last layer would
+    # draw its two hidden-dropout masks over compacted rows (kernels.BertLayerFn Tq), the fp8 runs'
+    # over the full layout
+    rows_on = K.ROWS["on"]
+    K.ROWS["on"] = False
+    try:
+        for name, m in (("bf16", m16), ("fp8", m8), ("fp8_dgrad", m8d)):
+            m.train()
+            opt = FusedAdamW(m.stores(), lr=1e-5, warmup=0, total_steps=10)
+            with K.fp8_forward(name != "bf16", training=True, dgrad=name == "fp8_dgrad"):
+                ls = []
+                for i in range(3):
+                    if i == 0:  # the first step's gradients, before the update
+                        m.zero_grad()
+                        m(inputs)[0].backward()
+                        grads[name] = torch.cat([s.grad.clone() for s in m.stores()])
+                        m.zero_grad()
+                    ls.append(float(train_step(m, opt, [inputs])))
+                if name != "bf16":
+                    assert len(K._FP8["cache"]) >= (32 if name == "fp8_dgrad" else 16)
+            losses[name] = ls
+    finally:
+        K.ROWS["on"] = rows_on
     print(f"config5 3-step losses: {losses}")
     for name in ("fp8", "fp8_dgrad"):
         for a, b in zip(losses[name], losses["bf16"]):
