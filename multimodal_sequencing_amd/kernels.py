@@ -235,9 +235,10 @@ ROWS = {"on": os.environ.get("MMSEQ_ROWS", "1") != "0"}
 class BertLayerFn(torch.autograd.Function):
     @staticmethod
     def rows_ok(x):
-        """The layer can run on the first Tq rows of every sequence only (forward(..., Tq)): bf16,
-        the variant-1 attention kernels (mmseq_attn_fwd_rows), no MX-fp8 path active."""
-        return ROWS["on"] and x.dtype == torch.bfloat16 and N._sel["attn"] == 1 and not _FP8["on"]
+        """The layer can run on the first Tq rows of every sequence only (forward(..., Tq)): bf16 and
+        the variant-1 attention kernels (mmseq_attn_fwd_rows). Under fp8_forward() that layer runs
+        in bf16 (its text rows are ~1/3 of the rows; the other layers keep the fp8 GEMMs)."""
+        return ROWS["on"] and x.dtype == torch.bfloat16 and N._sel["attn"] == 1
 
     @staticmethod
     def forward(ctx, x, key_bias, anchor, L, P, T, heads, eps, drops=(None, None, None), save=True,
