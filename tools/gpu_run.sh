@@ -14,6 +14,9 @@
 #   epi-ab:NAME      tools/gemm_epi_bench.py, NAME vs tree, twice     -> epi_{NAME,tree}.log
 #   bench-ab:NAME    short bench (config 3 only), NAME vs tree, twice -> bench_{NAME,tree}.log
 #   kstats:SCRIPT ARGS  rocprof kernel stats of python SCRIPT ARGS    -> <script>_stats.csv
+#   env-ab:VAR[:SCRIPT ARGS]  the short config-3 bench (or python SCRIPT ARGS) with VAR=0 vs VAR=1,
+#                    alternated twice (e.g. env-ab:MMSEQ_ROWS, env-ab:MMSEQ_ROWS:tools/c5_train.py bf16 3)
+#                                                                     -> envab_VAR{0,1}.log
 #   profile          tools/profile_round.sh TAG (kernel stats + PMC of the default bench)
 set -euo pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -65,6 +68,17 @@ for step in "$@"; do
     kstats)
       s=$(basename "${arg%% *}" .py)
       kstats "$out/${s}_stats.csv" $arg ;;
+    env-ab)
+      var=${arg%%:*}; cmd=""
+      [ "$var" != "$arg" ] && cmd=${arg#*:}
+      for v in 0 1 0 1; do
+        if [ -n "$cmd" ]; then
+          env "$var=$v" timeout -k 10 300 python3 $cmd >> "$out/envab_$var$v.log" 2>&1
+        else
+          env "$var=$v" timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 $short --fwd-steps 0 \
+            >> "$out/envab_$var$v.log" 2>&1
+        fi
+      done ;;
     profile)
       bash tools/profile_round.sh "$tag" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
