@@ -4,6 +4,7 @@
 //          (clip/model.py:262-278), with the per-pair image gather of
 //          process_images (process_inputs_for_berson.py:82-97) done on device.
 #include "common.h"
+#include <algorithm>
 
 mmseq_status ln_reduce_partials(int nb, int cols, const float* ws, float* dg, float* db,
                                 hipStream_t s);
@@ -13,6 +14,7 @@ namespace {
 
 constexpr int MAXV = 16;
 constexpr int RPB = 64;
+typedef unsigned short us;
 
 // ---------------------------------------------------------------------------------------------
 // text embeddings
@@ -143,18 +145,6 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
     ws_ln[((int64_t)blockIdx.x * 2 + 1) * H + c] =
         red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
   }
-}
-
-// dpos[t][c] += sum_p de[p][t][c], t >= 1 (position ids are 0..Lt-1, lxrt:358; row 0 = padding)
-__global__ __launch_bounds__(256) void embed_pos_kernel(int P, int Lt, int H,
-                                                        const float* __restrict__ de,
-                                                        float* __restrict__ dpos) {
-  const int t = blockIdx.y;
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (t == 0 || c >= H) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += de[((int64_t)p * Lt + t) * H + c];
-  dpos[(int64_t)t * H + c] += s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -385,7 +375,219 @@ __global__ __launch_bounds__(256) void vit_pos_kernel(int P, int ntok, int W, in
   dpos[(int64_t)r * W + c] += s;
 }
 
+// ---- bf16 ViT embedding, W = 256 NJ: half-wave rows, 16-byte accesses (the layout of
+// layernorm.hip's ln_fwd16 / ln_bwd16): lane l of a half-wave owns columns (j * 32 + l) * 8 .. +7
+__device__ __forceinline__ float hsum32(float v) {  // sum over the 32 lanes of a half-wave
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NJ>
+__global__ __launch_bounds__(256) void vit_embed_fwd16_kernel(int P, int ntok, int gg,
+                                                              const us* __restrict__ patch_out,
+                                                              const float* __restrict__ cls,
+                                                              const float* __restrict__ pos,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta,
+                                                              float eps, us* __restrict__ x,
+                                                              us* __restrict__ y,
+                                                              float* __restrict__ mean,
+                                                              float* __restrict__ rstd) {
+  constexpr int W = 256 * NJ;
+  const int l = threadIdx.x & 31;
+  const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (r >= (int64_t)P * ntok) return;
+  const int p = (int)(r / ntok), t = (int)(r - (int64_t)p * ntok);
+  const float* pr = pos + (int64_t)vit_pos_row(t, gg) * W;
+  const us* src = patch_out + ((int64_t)p * (ntok - 1) + (t > 0 ? t - 1 : 0)) * W;
+  u16x8 raw[NJ];
+  if (t > 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) raw[j] = *reinterpret_cast<const u16x8*>(src + (j * 32 + l) * 8);
+  }
+  // x = bf16(patch + pos) (the class row: bf16(cls + pos)); the statistics use the rounded values
+  // the backward re-reads
+  float v[NJ][8], s = 0.f;
+  us* xr = x + r * W;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (j * 32 + l) * 8;
+    const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + c), p1 = *reinterpret_cast<const f32x4*>(pr + c + 4);
+    float a[8];
+    if (t > 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = bf2f(raw[j][e]);
+    } else {
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cls + c), c1 = *reinterpret_cast<const f32x4*>(cls + c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = c0[e];
+        a[4 + e] = c1[e];
+      }
+    }
+    u16x8 xb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xb[e] = f2bf(a[e] + (e < 4 ? p0[e] : p1[e - 4]));
+      v[j][e] = bf2f(xb[e]);
+      s += v[j][e];
+    }
+    *reinterpret_cast<u16x8*>(xr + c) = xb;
+  }
+  const float mu = hsum32(s) / W;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[j][e] - mu;
+      q = fmaf(d, d, q);
+    }
+  const float rs = rsqrtf(hsum32(q) / W + eps);
+  us* yr = y + r * W;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (j * 32 + l) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c), g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c), b1 = *reinterpret_cast<const f32x4*>(beta + c + 4);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = f2bf(fmaf((v[j][e] - mu) * rs, g0[e], b0[e]));
+      o[4 + e] = f2bf(fmaf((v[j][4 + e] - mu) * rs, g1[e], b1[e]));
+    }
+    *reinterpret_cast<u16x8*>(yr + c) = o;
+  }
+  if (l == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+// backward of ln_pre + the embedding sum: RPB rows per block (8 half-waves, RPB / 8 rows each),
+// dx of the class rows to dx0 (fp32, [P][W]), of the patch rows to dpatch (bf16, the conv GEMM's
+// dY); per-block dgamma / dbeta partials -> ws_ln[block][2][W] (reduced in block order)
+template <int NJ>
+__global__ __launch_bounds__(256) void vit_embed_bwd16_kernel(int P, int ntok,
+                                                              const us* __restrict__ dy,
+                                                              const us* __restrict__ x,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ gamma,
+                                                              us* __restrict__ dpatch,
+                                                              float* __restrict__ dx0,
+                                                              float* __restrict__ ws_ln) {
+  constexpr int W = 256 * NJ;
+  __shared__ float red[4][2][W];
+  const int l = threadIdx.x & 31, hw = threadIdx.x >> 5;
+  const int64_t rows = (int64_t)P * ntok;
+  float pg[NJ][8], pb[NJ][8], gm[NJ][8];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (j * 32 + l) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c), g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gm[j][e] = g0[e];
+      gm[j][4 + e] = g1[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pg[j][e] = pb[j][e] = 0.f;
+  }
+  const int64_t rbeg = (int64_t)blockIdx.x * RPB;
+  for (int64_t r = rbeg + hw; r < rbeg + RPB && r < rows; r += 8) {
+    const int p = (int)(r / ntok), t = (int)(r - (int64_t)p * ntok);
+    const us* xr = x + r * W;
+    const us* dyr = dy + r * W;
+    u16x8 xa[NJ], da[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      xa[j] = *reinterpret_cast<const u16x8*>(xr + (j * 32 + l) * 8);
+      da[j] = *reinterpret_cast<const u16x8*>(dyr + (j * 32 + l) * 8);
+    }
+    const float mu = mean[r], rs = rstd[r];
+    float xh[NJ][8], gdy[NJ][8], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xv = (bf2f(xa[j][e]) - mu) * rs, d = bf2f(da[j][e]);
+        xh[j][e] = xv;
+        gdy[j][e] = d * gm[j][e];
+        pg[j][e] += d * xv;
+        pb[j][e] += d;
+        s1 += gdy[j][e];
+        s2 += gdy[j][e] * xv;
+      }
+    s1 = hsum32(s1) / W;
+    s2 = hsum32(s2) / W;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = (j * 32 + l) * 8;
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = rs * (gdy[j][e] - s1 - xh[j][e] * s2);
+      if (t == 0) {
+        float* o = dx0 + (int64_t)p * W + c;
+        *reinterpret_cast<f32x4*>(o) = (f32x4){d[0], d[1], d[2], d[3]};
+        *reinterpret_cast<f32x4*>(o + 4) = (f32x4){d[4], d[5], d[6], d[7]};
+      } else {
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(d[e]);
+        *reinterpret_cast<u16x8*>(dpatch + ((int64_t)p * (ntok - 1) + t - 1) * W + c) = o;
+      }
+    }
+  }
+  // the two half-waves of a wave own the same columns: combine them, then the 4 waves in order
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pg[j][e] += __shfl_xor(pg[j][e], 32, 64);
+      pb[j][e] += __shfl_xor(pb[j][e], 32, 64);
+    }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 32) == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = (j * 32 + l) * 8 + e;
+        red[wave][0][c] = pg[j][e];
+        red[wave][1][c] = pb[j][e];
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < W; c += 256) {
+    ws_ln[((int64_t)blockIdx.x * 2 + 0) * W + c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    ws_ln[((int64_t)blockIdx.x * 2 + 1) * W + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+  }
+}
+
+// dpos / dcls from the column sums over pairs: sp = sum_p dpatch[p] ((ntok - 1) x W), s0 = sum_p dx0[p]
+// (W); pos row r collects token r (r <= gg: the class row for r = 0) and token r + gg + 1 (r < gg)
+__global__ __launch_bounds__(256) void vit_pos_fold_kernel(int W, int gg, const float* __restrict__ sp,
+                                                           const float* __restrict__ s0,
+                                                           float* __restrict__ dcls,
+                                                           float* __restrict__ dpos) {
+  const int r = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= W) return;
+  if (r == gg + 1) {
+    dcls[c] += s0[c];
+    return;
+  }
+  float v = r == 0 ? s0[c] : sp[(int64_t)(r - 1) * W + c];
+  if (r < gg) v += sp[(int64_t)(r + gg) * W + c];
+  dpos[(int64_t)r * W + c] += v;
+}
+
 }  // namespace
+
+extern "C" mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t ldx, float* out,
+                                     int accumulate, float* ws, mmseq_dtype dt, mmseq_stream stream);
+extern "C" int64_t mmseq_colsum_workspace(int rows, int cols);
 
 extern "C" mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* ids,
                                            const int64_t* tt, const float* word, const float* pos,
@@ -414,7 +616,9 @@ extern "C" mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* 
 extern "C" int64_t mmseq_embed_ln_bwd_workspace(int P, int Lt, int H) {
   const int64_t rows = (int64_t)P * Lt;
   const int nb = (int)((rows + RPB - 1) / RPB);
-  return rows * H + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H);
+  // de | LN partials + reduction scratch | the column-sum scratch of dpos
+  const int64_t cs = Lt > 1 ? mmseq_colsum_workspace(P, (Lt - 1) * H) : 0;
+  return rows * H + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H) + cs;
 }
 
 extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* ids,
@@ -441,10 +645,15 @@ extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* 
     hipLaunchKernelGGL(embed_bwd_kernel<unsigned short>, dim3(nb), dim3(256), 0, s, P, Lt, H, ids,
                        tt, word, pos, type, gamma, mean, rstd, (const unsigned short*)djoint,
                        ld_pair, dword, dtype_tab, ws_de, ws_ln, make_drop(drop));
-  hipLaunchKernelGGL(embed_pos_kernel, dim3((H + 255) / 256, Lt), dim3(256), 0, s, P, Lt, H,
-                     ws_de, dpos);
   mmseq_status st = mmseq_check_launch("embed_ln_bwd");
   if (st) return st;
+  // dpos[t] += sum_p de[p][t] for t >= 1 (row 0 = padding_idx): a deterministic column sum over the
+  // P pairs of de viewed as [P][Lt * H] (a sequential loop over P per column was latency-bound)
+  if (Lt > 1) {
+    float* cws = ws_ln + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H);
+    st = mmseq_colsum(P, (Lt - 1) * H, ws_de + H, (int64_t)Lt * H, dpos + H, 1, cws, MMSEQ_F32, stream);
+    if (st) return st;
+  }
   return ln_reduce_partials(nb, H, ws_ln, dgamma, dbeta, s);
 }
 
@@ -472,6 +681,13 @@ extern "C" mmseq_status mmseq_vit_im2col(int B, int N, int npair, int R, int ps,
   return mmseq_check_launch("vit_im2col");
 }
 
+static bool vit_vec16(const void* a, const void* b, const void* c, const void* d, const void* e,
+                      const void* f, const void* g) {
+  const uintptr_t o = (uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)d | (uintptr_t)e |
+                      (uintptr_t)f | (uintptr_t)g;
+  return (o & 15) == 0;
+}
+
 extern "C" mmseq_status mmseq_vit_embed_fwd(int P, int ntok, int W, int npatch_img,
                                             const void* patch_out, const float* cls,
                                             const float* pos, const float* gamma,
@@ -482,6 +698,14 @@ extern "C" mmseq_status mmseq_vit_embed_fwd(int P, int ntok, int W, int npatch_i
                 "vit_embed: requires img_len = 2 (ntok = 1 + 2*npatch) and W <= 1024");
   if (P == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MMSEQ_BF16 && W % 256 == 0 && vit_vec16(patch_out, x, y, cls, pos, gamma, beta)) {
+    const dim3 g8((unsigned)(((int64_t)P * ntok + 7) / 8));
+#define VEF(NJ) hipLaunchKernelGGL(vit_embed_fwd16_kernel<NJ>, g8, dim3(256), 0, s, P, ntok, npatch_img, \
+                                   (const us*)patch_out, cls, pos, gamma, beta, eps, (us*)x, (us*)y, mean, rstd)
+    switch (W / 256) { case 1: VEF(1); break; case 2: VEF(2); break; case 3: VEF(3); break; default: VEF(4); }
+#undef VEF
+    return mmseq_check_launch("vit_embed_fwd");
+  }
   dim3 grid((unsigned)(((int64_t)P * ntok + 3) / 4));
   if (dtype == MMSEQ_F32)
     hipLaunchKernelGGL(vit_embed_fwd_kernel<float>, grid, dim3(256), 0, s, P, ntok, W, npatch_img,
@@ -497,7 +721,10 @@ extern "C" mmseq_status mmseq_vit_embed_fwd(int P, int ntok, int W, int npatch_i
 extern "C" int64_t mmseq_vit_embed_bwd_workspace(int P, int ntok, int W) {
   const int64_t rows = (int64_t)P * ntok;
   const int nb = (int)((rows + RPB - 1) / RPB);
-  return (int64_t)P * W + (int64_t)nb * 2 * W + mmseq_reduce_extra(nb, 2 * W);
+  // dx0 | LN partials + their reduction scratch | (bf16 path) sums over pairs of dpatch and dx0 +
+  // the column-sum scratch
+  const int64_t cs = std::max(mmseq_colsum_workspace(P, (ntok - 1) * W), mmseq_colsum_workspace(P, W));
+  return (int64_t)P * W + (int64_t)nb * 2 * W + mmseq_reduce_extra(nb, 2 * W) + (int64_t)ntok * W + cs;
 }
 
 extern "C" mmseq_status mmseq_vit_embed_bwd(int P, int ntok, int W, int npatch_img,
@@ -521,6 +748,27 @@ extern "C" mmseq_status mmseq_vit_embed_bwd(int P, int ntok, int W, int npatch_i
                        dx0, ws_ln);
     hipLaunchKernelGGL(vit_pos_kernel<float>, gpos, dim3(256), 0, s, P, ntok, W, npatch_img,
                        (const float*)dpatch_out, dx0, dcls, dpos);
+  } else if (W % 256 == 0 && vit_vec16(dy, x, dpatch_out, gamma, dx0, nullptr, nullptr)) {
+    // 16-byte rows; dpos / dcls from deterministic column sums over the P pairs (a sequential loop
+    // over P per column was latency-bound: 557 us at config 3)
+#define VEB(NJ) hipLaunchKernelGGL(vit_embed_bwd16_kernel<NJ>, dim3(nb), dim3(256), 0, s, P, ntok, \
+                                   (const us*)dy, (const us*)x, mean, rstd, gamma, (us*)dpatch_out, dx0, ws_ln)
+    switch (W / 256) { case 1: VEB(1); break; case 2: VEB(2); break; case 3: VEB(3); break; default: VEB(4); }
+#undef VEB
+    mmseq_status st = mmseq_check_launch("vit_embed_bwd");
+    if (st) return st;
+    float* sp = ws_ln + (int64_t)nb * 2 * W + mmseq_reduce_extra(nb, 2 * W);  // [(ntok - 1)][W]
+    float* s0 = sp + (int64_t)(ntok - 1) * W;                                   // [W]
+    float* cws = s0 + W;
+    st = mmseq_colsum(P, (ntok - 1) * W, dpatch_out, (int64_t)(ntok - 1) * W, sp, 0, cws, MMSEQ_BF16,
+                      stream);
+    if (st) return st;
+    st = mmseq_colsum(P, W, dx0, W, s0, 0, cws, MMSEQ_F32, stream);
+    if (st) return st;
+    hipLaunchKernelGGL(vit_pos_fold_kernel, gpos, dim3(256), 0, s, W, npatch_img, sp, s0, dcls, dpos);
+    st = mmseq_check_launch("vit_pos_fold");
+    if (st) return st;
+    return ln_reduce_partials(nb, W, ws_ln, dgamma, dbeta, s);
   } else {
     hipLaunchKernelGGL(vit_embed_bwd_kernel<unsigned short>, dim3(nb), dim3(256), 0, s, P, ntok,
                        W, (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,

@@ -439,9 +439,12 @@ def test_embed_ln_fwd_bwd(dtype):
     assert dw.abs().sum() > 0
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_vit_im2col_embed_fwd_bwd(dtype):
-    B, Nst, R, ps, W = 2, 3, 32, 8, 64
+@pytest.mark.parametrize("dtype,W", [(torch.float32, 64), (torch.bfloat16, 64), (torch.bfloat16, 768),
+                                     (torch.bfloat16, 1024)])
+def test_vit_im2col_embed_fwd_bwd(dtype, W):
+    """W = 64: the generic kernels; bf16 with W % 256 == 0: the 16-byte half-wave kernels and dpos /
+    dcls from column sums over the pairs (config 3 / 5 widths)."""
+    B, Nst, R, ps = 2, 3, 32, 8
     g = torch.Generator(device="cpu").manual_seed(6)
     images = torch.randn(B, Nst, 3, R, R, generator=g).to(DEV)
     pairs = torch.tensor([[[0, 1], [2, 0]], [[1, 2], [2, 1]]], device=DEV)
