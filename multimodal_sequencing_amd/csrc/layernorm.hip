@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256) void ln_fwd16_q8_kernel(int rows, int cols,
   }
 }
 
-// dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres); RPB16 rows per block,
+// dx = rstd * (g*dy - mean_c(g*dy) - xhat * mean_c(g*dy*xhat)) (+ dres); rpb rows per block,
 // each half wave walks rows hw, hw + 8, ... with the next row's loads issued before the current
 // row's math; per-block dgamma / dbeta partials -> ws[block][2][cols]
 constexpr int RPB16 = 64;
@@ -374,7 +374,7 @@ constexpr int RPB16 = 64;
 // dx with the residual) also leaves in MX-fp8 (mmseq_quant_mxfp8 of the bf16 values: q [rows][ldq],
 // packed scales; the padding rows' scales are the caller's, zero-initialised)
 template <int NJ, bool DIN, bool DXD, bool Q8 = false>
-__global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const us* __restrict__ dy,
+__global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, int rpb, const us* __restrict__ dy,
                                                        mmseq_rows dyl, const us* __restrict__ x,
                                                        mmseq_rows xl, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
@@ -392,8 +392,8 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, const
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) pg[j][e] = pb[j][e] = 0.f;
-  const int64_t rbeg = (int64_t)blockIdx.x * RPB16;
-  const int64_t rend = rbeg + RPB16 < rows ? rbeg + RPB16 : rows;
+  const int64_t rbeg = (int64_t)blockIdx.x * rpb;
+  const int64_t rend = rbeg + rpb < rows ? rbeg + rpb : rows;
   auto load_g = [&](int c, float* g8) {
     const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c), g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
 #pragma unroll
@@ -619,13 +619,19 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
   if (dtype == MMSEQ_BF16 && cols % 256 == 0 && cols <= 1024 && rows_vec16(dy, dyl) && rows_vec16(x, xl) &&
       rows_vec16(dx, dxl) && (!dres || rows_vec16(dres, dresl)) &&
       (!dx_drop || rows_vec16(dx_drop, dxdl)) && ((uintptr_t)gamma % 16) == 0) {
-    const int nb16 = (rows + RPB16 - 1) / RPB16;
+    // at most 512 blocks (two per CU at this kernel's ~190 VGPRs: one resident round), each over
+    // rpb rows: 2.5-10x fewer dgamma / dbeta partial rows to write and reduce than 64-row blocks
+    int rpb = RPB16, nb16 = (rows + RPB16 - 1) / RPB16;
+    if (nb16 > 512) {
+      rpb = ((rows + 511) / 512 + 7) / 8 * 8;
+      nb16 = (rows + rpb - 1) / rpb;
+    }
     const bool di = din.thr != 0, dd = dx_drop != nullptr;
 #define LNB16K(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B>), dim3(nb16), dim3(256), 0, s, rows, \
-                    cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,         \
+                    cols, rpb, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,         \
                     (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, nullptr, 0, nullptr)
 #define LNB16Q(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B, true>), dim3(nb16), dim3(256), 0, s, \
-                    rows, cols, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,   \
+                    rows, cols, rpb, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,   \
                     (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, (uint8_t*)q, ldq, \
                     (uint8_t*)q_scales)
 #define LNB16(NJ)                                           \
