@@ -906,7 +906,8 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
     const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
     int S2 = t256 < g_num_cu ? g_num_cu / t256 : 1;
     if (S2 > K / 1024) S2 = K / 1024 > 0 ? K / 1024 : 1;
-    const int64_t cs_rows = bias_grad ? M : 0;
+    const int tn256 = (N + 255) / 256;
+    const int64_t cs_rows = bias_grad ? (int64_t)tn256 * M : 0;  // one partial row per column tile
     while (S2 > 1 && (!g_slab || (int64_t)S2 * (cs_rows + (int64_t)M * N) * 4 > g_slab_bytes)) --S2;
     t.splitk = S2;
     t.kchunk = ((K + S2 - 1) / S2 + 127) / 128 * 128;
@@ -914,7 +915,12 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
     if (t.splitk <= 1) { t.splitk = 1; t.kchunk = K; }
     t.slab = g_slab;
     t.cs = bias_grad;
-    t.cs_slab = t.splitk > 1 && bias_grad ? g_slab + (int64_t)t.splitk * M * N : nullptr;
+    // the bias gradient's partials [split][column tile][M] (balanced over the column tiles, summed
+    // in fixed order by cs_reduce); without workspace room the first column tile adds them directly
+    const int64_t slab_c = t.splitk > 1 ? (int64_t)t.splitk * M * N : 0;
+    t.cs_slab = bias_grad && g_slab &&
+                        (slab_c + (int64_t)t.splitk * tn256 * M) * 4 <= g_slab_bytes
+                    ? g_slab + slab_c : nullptr;
     hipError_t e2 = hipSuccess;
     if (mmseq_gemm256_tn(t, s, &e2)) {
       if (e2 == hipSuccess && t.splitk > 1) {
@@ -922,9 +928,11 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
         const unsigned blocks = (unsigned)((t4 + 255) / 256 < 4096 ? (t4 + 255) / 256 : 4096);
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, M, N, t.splitk,
                            g_slab, C, ldc, 1);
-        if (bias_grad)
-          hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, t.splitk,
-                             t.cs_slab, bias_grad);
+        e2 = hipGetLastError();
+      }
+      if (e2 == hipSuccess && t.cs_slab) {
+        hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M,
+                           t.splitk * tn256, t.cs_slab, bias_grad);
         e2 = hipGetLastError();
       }
       if (e2 != hipSuccess) return mmseq_set_error(MMSEQ_EHIP, "gemm_wgrad: %s", hipGetErrorString(e2));

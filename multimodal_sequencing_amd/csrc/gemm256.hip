@@ -757,17 +757,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   bf16x8_t fa[8], fb[4];
-  // fused bias gradient (column sums of A = dY): blocks of the first column tile only; wave wc
-  // sums A tiles i = wc (cs0) and 4 + wc (cs1) on the VALU beside its MFMAs; lane (g, ii) holds
-  // the partial over its k-slots of column wr*128 + i*16 + ii
-  const bool do_cs = a.cs != nullptr && tn == 0;
+  // fused bias gradient (column sums of A = dY): wave wc sums A tiles i = wc (cs0) and 4 + wc
+  // (cs1) on the VALU beside its MFMAs; lane (g, ii) holds the partial over its k-slots of column
+  // wr*128 + i*16 + ii. With a partial slab (a.cs_slab) the tiles_n blocks that share an M-tile
+  // split the work by K-tile (K-tile k goes to column tile k % tiles_n) and each writes its own
+  // partial row [split * tiles_n + tn], so no block is slower than the others; without one, the
+  // first column tile's blocks do it all (a.cs += directly).
+  const bool cs_split = a.cs_slab != nullptr;
+  const bool do_cs = a.cs != nullptr && (cs_split || tn == 0);
   float cs0 = 0.f, cs1 = 0.f;
-  bf16x8_t fcs;  // the wave's bias-gradient fragment: one extra transposed read per phase
-  const int fAc0 = kr * 256 + (((wr * 16 + 2 * wc + (pp >> 1)) ^ (t8 << 1)) << 3) + (pp & 1) * 4;
-  const int fAc1 = kr * 256 + (((wr * 16 + 2 * (4 + wc) + (pp >> 1)) ^ (t8 << 1)) << 3) + (pp & 1) * 4;
-  auto cs_add = [&](float& dst) {
+  // the summed fragment is the MFMA's own A fragment fa[I0 + wc] of the phase (no extra LDS read
+  // or register: a separate transposed read of it held 4 more VGPRs in a kernel at 256)
+  auto cs_add = [&](float& dst, const bf16x8_t& f) {
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-    const u32x4 u = __builtin_bit_cast(u32x4, fcs);
+    const u32x4 u = __builtin_bit_cast(u32x4, f);
     float t = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) t += __uint_as_float(u[e] << 16) + __uint_as_float(u[e] & 0xFFFF0000u);
@@ -782,19 +785,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
 
 #define TN_PHASE(READS, STAGE, VMWAIT, I0, KS)                                          \
   READS;                                                                                \
-  if (do_cs) fcs = frag(buf + (KS) * 32 * 256 + ((I0) ? fAc1 : fAc0));                  \
   STAGE;                                                                                \
   __builtin_amdgcn_sched_barrier(0);                                                    \
   if (VMWAIT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                          \
   __builtin_amdgcn_s_barrier();                                                         \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                    \
+  if (do_cs && my_k) {  /* wave-uniform wc: a scalar branch, static fragment indices; */ \
+    /* summed before the MFMAs so that no fragment outlives them */                       \
+    if (wc == 0) cs_add((I0) ? cs1 : cs0, fa[(I0) + 0]);                                  \
+    else if (wc == 1) cs_add((I0) ? cs1 : cs0, fa[(I0) + 1]);                             \
+    else if (wc == 2) cs_add((I0) ? cs1 : cs0, fa[(I0) + 2]);                             \
+    else cs_add((I0) ? cs1 : cs0, fa[(I0) + 3]);                                          \
+  }                                                                                       \
   __builtin_amdgcn_sched_barrier(0);                                                    \
   __builtin_amdgcn_s_setprio(1);                                                        \
   _Pragma("unroll") for (int i = I0; i < I0 + 4; ++i)                                   \
   _Pragma("unroll") for (int j = 0; j < 4; ++j)                                         \
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);                                                        \
-  if (do_cs) cs_add((I0) ? cs1 : cs0);                                                  \
   __builtin_amdgcn_sched_barrier(0);                                                    \
   __builtin_amdgcn_s_barrier();
 
@@ -802,6 +810,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int buf = h * (2 * G_LDA_HALF);
+      const bool my_k = !cs_split || (2 * s + h) % tiles_n == tn;  // block-uniform
       // phase 1 (5): ks0, i 0-3
       TN_PHASE(
           { _Pragma("unroll") for (int i = 0; i < 4; ++i) fa[i] = frag(buf + fA[i]);
@@ -835,7 +844,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(GemmArgs a, int tile
         const int m = m0 + wr * 128 + (q * 4 + wc) * 16 + ii;
         const float v = q ? cs1 : cs0;
         if (m < a.M) {
-          if (a.splitk > 1) a.cs_slab[(int64_t)split * a.M + m] = v;
+          if (cs_split) a.cs_slab[((int64_t)split * tiles_n + tn) * a.M + m] = v;
           else a.cs[m] += v;
         }
       }

@@ -15,7 +15,7 @@ struct GemmArgs {
   int splitk; int kchunk; float* slab;  // split-K (TN wgrad): partial slabs [splitk][M][N] f32
   Drop drop;                            // dropout after the activation, before the residual
   float* cs;       // TN wgrad: fused bias gradient cs[m] += sum_k A[k][m] (nullptr: off)
-  float* cs_slab;  // ... per-split partials [splitk][M] when splitk > 1
+  float* cs_slab;  // ... its partials [splitk][column tile][M] (nullptr: first column tile adds to cs)
   uint8_t* q8_scales;  // 256 NT kernel, MX-fp8 output: C is e4m3 [M][ldc] + these packed scales
   // 256 NT kernel, MX-fp8 operands (F8): A / B are e4m3 [rows][ld] with these packed E8M0 scales
   const uint8_t* f8_sa; const uint8_t* f8_sb; int64_t f8_sa_bytes, f8_sb_bytes;
