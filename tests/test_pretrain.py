@@ -145,9 +145,18 @@ def test_pretrain_bf16_close_to_reference():
 
 # ---- config 2 at its stated size (tests/golden/pretrain_real: ViT-B/16 at 224^2, H = 768,
 # bert-base-uncased vocab 30522, B = 2 stories; reference outputs only, see the generator) ------
-def _sample_check(d, grads, fp32):
-    """Per-parameter gradient norm and the 2 x 1024 recorded samples (make_golden_real.grad_samples)."""
+def _sample_check(d, grads, fp32, stories=2):
+    """Per-parameter gradient norm and the 2 x 1024 recorded samples (make_golden_real.grad_samples).
+
+    An analytically zero gradient (the MRM decoder's shared bias: the column sum of softmax - onehot)
+    is rounding noise. In fp32 it stays below 1e-4 of the total gradient norm. In bf16 the column
+    sum runs over the bf16-rounded score gradients (the backward of scores.float()), each off by at
+    most 2^-9 relative, and sum |d scores| <= 2 * MRM_SCALE per story (mean CE over the nm rows of
+    a story, each row's |softmax - onehot|_1 <= 2), so |g| <= 2^-9 * 2 * 0.2 * stories."""
     from make_golden_real import grad_samples
+    zero_bound = 1e-4 * float(d["grad_norm"])
+    if not fp32:
+        zero_bound = max(zero_bound, 2.0 ** -9 * 2 * 0.2 * stories)
     checked = 0
     for k in d:
         if not k.startswith("gn::"):
@@ -160,7 +169,7 @@ def _sample_check(d, grads, fp32):
         h, s = grad_samples(g)
         if ref_n < 1e-6 * float(d["grad_norm"]):  # exactly or analytically zero (a softmax-CE
             # shared bias): rounding noise on both sides
-            assert float(np.linalg.norm(g)) < 1e-4 * float(d["grad_norm"]), name
+            assert float(np.linalg.norm(g)) < zero_bound, name
             checked += 1
             continue
         if fp32:
