@@ -610,14 +610,24 @@ __global__ __launch_bounds__(256, 2) void gemm_ring_kernel(GemmArgs a, int tiles
 }
 
 // C[m][n] (+)= sum_s slab[s][m][n], fixed order (bitwise reproducible)
-// out[m] += sum_s slab[s][m] (fused bias-gradient partials of the split-K wgrad; fixed order)
+// out[m] += sum_s slab[s][m] (fused bias-gradient partials of the split-K wgrad; fixed order).
+// S = splits x column tiles runs to ~100 partials: a block takes 32 columns and spreads the
+// partials over 8 slices (slice j sums s = j, j + 8, ...), then adds the 8 slice sums in order
 __global__ __launch_bounds__(256) void cs_reduce_kernel(int M, int S, const float* __restrict__ slab,
                                                         float* __restrict__ out) {
-  const int m = blockIdx.x * 256 + threadIdx.x;
-  if (m >= M) return;
+  __shared__ float red[8][32];
+  const int c = threadIdx.x & 31, j = threadIdx.x >> 5;
+  const int m = blockIdx.x * 32 + c;
   float v = 0.f;
-  for (int s = 0; s < S; ++s) v += slab[(int64_t)s * M + m];
-  out[m] += v;
+  if (m < M) {
+#pragma unroll 4
+    for (int s = j; s < S; s += 8) v += slab[(int64_t)s * M + m];
+  }
+  red[j][c] = v;
+  __syncthreads();
+  if (j == 0 && m < M)
+    out[m] += ((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) +
+              ((red[4][c] + red[5][c]) + (red[6][c] + red[7][c]));
 }
 
 // out[m] += sum_k A[k][m] (fallback bias gradient when the fused path is not eligible)
@@ -855,7 +865,7 @@ extern "C" int64_t mmseq_gemm_workspace_size(int M, int N, int K) {
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   int64_t s2 = t256 < cus ? cus / t256 : 1;
   if (s2 > K / 1024) s2 = K / 1024 > 0 ? K / 1024 : 1;
-  if (s2 > 1) best = s2 * (M + MN) * 4;
+  if (s2 > 1) best = s2 * ((int64_t)((N + 255) / 256) * M + MN) * 4;  // + bias partials per column tile
   const int64_t tiles = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (tiles < 512) {
     int64_t s = (1024 + tiles - 1) / tiles;
@@ -931,7 +941,7 @@ extern "C" mmseq_status mmseq_gemm_wgrad(int M, int N, int K, const void* A, int
         e2 = hipGetLastError();
       }
       if (e2 == hipSuccess && t.cs_slab) {
-        hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M,
+        hipLaunchKernelGGL(cs_reduce_kernel, dim3((M + 31) / 32), dim3(256), 0, s, M,
                            t.splitk * tn256, t.cs_slab, bias_grad);
         e2 = hipGetLastError();
       }
