@@ -17,6 +17,8 @@
 #   env-ab:VAR[:SCRIPT ARGS]  the short config-3 bench (or python SCRIPT ARGS) with VAR=0 vs VAR=1,
 #                    alternated twice (e.g. env-ab:MMSEQ_ROWS, env-ab:MMSEQ_ROWS:tools/c5_train.py bf16 3)
 #                                                                     -> envab_VAR{0,1}.log
+#   lib-ab:NAME:SCRIPT ARGS  python SCRIPT ARGS with ab/libmmseq_NAME.so vs the tree, alternated
+#                    twice (e.g. lib-ab:base:tools/ln_bench.py bwd)   -> <script>_{NAME,tree}.log
 #   profile          tools/profile_round.sh TAG (kernel stats + PMC of the default bench)
 set -euo pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -79,6 +81,14 @@ for step in "$@"; do
             >> "$out/envab_$var$v.log" 2>&1
         fi
       done ;;
+    lib-ab)
+      lname=${arg%%:*}; cmd=${arg#*:}
+      s=$(basename "${cmd%% *}" .py)
+      for v in "$lname" tree "$lname" tree; do
+        with_lib "$v"
+        timeout -k 10 300 python3 $cmd >> "$out/${s}_$v.log" 2>&1
+      done
+      unset MMSEQ_BENCH_LIB ;;
     profile)
       bash tools/profile_round.sh "$tag" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
