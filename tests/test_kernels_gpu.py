@@ -233,7 +233,8 @@ def test_attention_rescale_and_zero_bias_tiles(profile, bias_mode, fast):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,cols,eps", [(100, 768, 1e-12), (7, 128, 1e-5), (300, 96, 1e-6),
-                                           (64, 1536, 1e-12), (33, 2048, 1e-5), (17, 1100, 1e-6)])
+                                           (64, 1536, 1e-12), (33, 2048, 1e-5), (17, 1100, 1e-6),
+                                           (70001, 768, 1e-12)])  # > 512 blocks: rpb > 64
 def test_layernorm(dtype, rows, cols, eps):
     g = torch.Generator(device="cpu").manual_seed(rows + cols)
     x = (torch.randn(rows, cols, generator=g) * 2 + 0.5).to(DEV, dtype)
