@@ -10,6 +10,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodal_sequencing_amd import _native as N  # noqa: E402
 from yardstick import timed  # noqa: E402
+if os.environ.get("MMSEQ_BENCH_LIB"):  # A/B of library builds (tools/gpu_run.sh lib-ab)
+    N.LIB_PATH = os.environ["MMSEQ_BENCH_LIB"]
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 640 * 513
 g = torch.Generator(device="cuda").manual_seed(0)
