@@ -264,7 +264,9 @@ mmseq_status mmseq_layernorm_bwd_rows(int rows, int cols, const void* dy, mmseq_
  * lxrt/modeling.py:356-370; joint concat :1093): for pair p, token t < Lt:
  *   e = word[ids] + pos[t] + type[tt];  joint row (p*ld_pair + t) = LN(e)   (eps as given)
  * bwd recomputes e, applies LN backward and scatters into dword/dpos/dtype (+=), skipping
- * row 0 of every table (padding_idx = 0 on all three, :347-349). dgamma/dbeta accumulate.
+ * row 0 of every table (padding_idx = 0 on all three, :347-349). dgamma/dbeta accumulate. Every
+ * table row's sum runs in a fixed order (rows grouped by id with a radix sort, summed in row
+ * order; no float atomics), so the backward is bit-stable run to run. ids must be < 2^32 - 1.
  * drop: embedding dropout (:369) on the LN output, idx = (p*Lt + t)*H + c.
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* ids, const int64_t* tt,
@@ -354,8 +356,9 @@ mmseq_status mmseq_adamw(int64_t n, float* p, const float* g, float* m, float* v
  *   (w_bias is a device pointer, may be NULL)
  *   e = -1e9 where pointed[b][t][j] != 0 or j >= tgt_len[b];  logp = log_softmax_j(e)
  *   nll[b][t] = -logp[b][t][target[b][t]] if t < tgt_len[b] else 0
- * bwd: given dnll[b][t] (upstream grad of each nll) WRITE dq, dkey and ACCUMULATE (+=, float
- * atomics) dokey, dw, dw_bias. Shapes: q [B][N][H], key [B][N][N][H], okey [B][N][H] (f32).
+ * bwd: given dnll[b][t] (upstream grad of each nll) WRITE dq, dkey and ACCUMULATE (+=) dokey, dw,
+ * dw_bias, every sum in a fixed order (bit-stable run to run). Shapes: q [B][N][H],
+ * key [B][N][N][H], okey [B][N][H] (f32); workspace: mmseq_pointer_bwd_workspace(B, N, H) floats.
  * ------------------------------------------------------------------------------------------ */
 mmseq_status mmseq_pointer_fwd(int B, int N, int H, const float* q, const float* key,
                                const float* okey, const float* w, const float* w_bias,
@@ -366,7 +369,8 @@ mmseq_status mmseq_pointer_bwd(int B, int N, int H, const float* q, const float*
                                const float* okey, const float* w, const float* logp,
                                const uint8_t* pointed, const int64_t* tgt_len, const int64_t* target, const float* dnll,
                                float* dq, float* dkey, float* dokey, float* dw, float* dw_bias,
-                               mmseq_stream stream);
+                               float* workspace, mmseq_stream stream);
+int64_t mmseq_pointer_bwd_workspace(int B, int N, int H);
 
 /* ------------------------------------------------------------------------------------------
  * HierarchicalAttention span pooling (modeling_bert.py:703-741) without host loops:

@@ -138,7 +138,8 @@ _SIGS = {
     "mmseq_adamw": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp] + [ctypes.c_float] * 5 +
                     [ctypes.c_int, ctypes.c_float, _vp, _vp, _vp]),
     "mmseq_pointer_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 5 + [_vp] * 5 + [_vp]),
-    "mmseq_pointer_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 14 + [_vp]),
+    "mmseq_pointer_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp] * 15 + [_vp]),
+    "mmseq_pointer_bwd_workspace": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_span_pool_fwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
                                                                 ctypes.c_int, _dp, _vp]),
     "mmseq_span_pool_bwd": (ctypes.c_int, [ctypes.c_int] * 3 + [_vp, _c_i64, _vp, _vp, _vp, _vp,
@@ -498,9 +499,10 @@ def pointer_fwd(B, N, H, q, key, okey, w, wb, pointed, tgt_len, target, logp, nl
 
 def pointer_bwd(B, N, H, q, key, okey, w, logp, pointed, tgt_len, target, dnll, dq, dkey, dokey,
                 dw, dwb):
+    ws = torch.empty(lib().mmseq_pointer_bwd_workspace(B, N, H), dtype=torch.float32, device=q.device)
     _check(lib().mmseq_pointer_bwd(B, N, H, _p(q), _p(key), _p(okey), _p(w), _p(logp),
                                    _p(pointed), _p(tgt_len), _p(target), _p(dnll), _p(dq), _p(dkey),
-                                   _p(dokey), _p(dw), _p(dwb), _stream()), "mmseq_pointer_bwd")
+                                   _p(dokey), _p(dw), _p(dwb), _p(ws), _stream()), "mmseq_pointer_bwd")
 
 
 def span_pool_fwd(P, Lt, H, top, ld_pair, score, sep, probs, mix, drop=None):

@@ -5,6 +5,7 @@
 //          process_images (process_inputs_for_berson.py:82-97) done on device.
 #include "common.h"
 #include <algorithm>
+#include <rocprim/device/device_radix_sort.hpp>
 
 mmseq_status ln_reduce_partials(int nb, int cols, const float* ws, float* dg, float* db,
                                 hipStream_t s);
@@ -67,8 +68,10 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(int P, int Lt, int H,
   }
 }
 
-// LN backward on recomputed e; de -> ws_de [P*Lt][H] (f32); word/type scatter with atomics
-// (row 0 skipped: padding_idx = 0 on all three tables, lxrt/modeling.py:347-349).
+// LN backward on recomputed e; de -> ws_de [P*Lt][H] (f32). The word / type tables' scatter-add
+// runs afterwards in a fixed order (table_scatter_det: rows grouped by id, summed in row order), so
+// the backward is bit-stable run to run (row 0 skipped: padding_idx = 0 on all three tables,
+// lxrt/modeling.py:347-349).
 template <typename T>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
                                                         const int64_t* __restrict__ ids,
@@ -80,8 +83,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd,
                                                         const T* __restrict__ djoint,
-                                                        int64_t ld_pair, float* __restrict__ dword,
-                                                        float* __restrict__ dtype_tab,
+                                                        int64_t ld_pair,
                                                         float* __restrict__ ws_de,
                                                         float* __restrict__ ws_ln, Drop dr) {
   __shared__ float red[4][2][1024];
@@ -125,8 +127,6 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
       if (c < H) {
         float de = rs * (gdy[j] - s1 - xh[j] * s2);
         ws_de[r * H + c] = de;
-        if (id != 0) atomicAdd(dword + id * H + c, de);
-        if (ty != 0 && dtype_tab) atomicAdd(dtype_tab + ty * H + c, de);
       }
     }
   }
@@ -145,6 +145,120 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int P, int Lt, int H,
     ws_ln[((int64_t)blockIdx.x * 2 + 1) * H + c] =
         red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deterministic embedding-table gradient: table[id] += sum of de[r] over the rows r with ids[r] ==
+// id (id 0 skipped, padding_idx), every sum in ascending row order. The rows are grouped by one
+// radix sort of the keys (id << 32 | r); the sorted positions are cut into chunks of SEG_C, one
+// workgroup per chunk sums each run of equal ids in order; a run wholly inside its chunk is added
+// to the table by that workgroup, a run crossing chunk boundaries leaves its pieces in per-chunk
+// slots that the segment's first chunk then adds in chunk order. Replaces float atomics, whose
+// ordering made two backwards of the same inputs differ.
+// ---------------------------------------------------------------------------------------------
+constexpr int SEG_C = 64;
+constexpr uint32_t SEG_NONE = 0xFFFFFFFFu;  // an id no row has (ids < 2^32 - 1)
+
+__global__ __launch_bounds__(256) void row_keys_kernel(int64_t n, const int64_t* __restrict__ ids,
+                                                       uint64_t* __restrict__ keys) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r < n) keys[r] = ((uint64_t)(uint32_t)ids[r] << 32) | (uint64_t)(uint32_t)r;
+}
+
+__device__ __forceinline__ uint32_t seg_id(const uint64_t* keys, int64_t n, int64_t i) {
+  return (i >= 0 && i < n) ? (uint32_t)(keys[i] >> 32) : SEG_NONE;
+}
+
+// one workgroup per chunk of SEG_C sorted positions; thread t owns columns 4t .. 4t + 3 (H <= 1024,
+// H % 4 == 0); parts [nch][2][H]: slot 0 = the chunk's first run when it continues a run of the
+// previous chunk, slot 1 = its last run when that run starts here and continues into the next chunk
+__global__ __launch_bounds__(256) void seg_rows_kernel(int64_t n, int H, const uint64_t* __restrict__ keys,
+                                                       const float* __restrict__ de,
+                                                       float* __restrict__ table,
+                                                       float* __restrict__ parts) {
+  __shared__ uint64_t k[SEG_C];
+  const int64_t c = blockIdx.x, i0 = c * SEG_C;
+  const int cnt = (int)min((int64_t)SEG_C, n - i0);
+  const int tid = threadIdx.x;
+  if (tid < cnt) k[tid] = keys[i0 + tid];
+  __syncthreads();
+  const uint32_t prev = seg_id(keys, n, i0 - 1), next = seg_id(keys, n, i0 + cnt);
+  const bool act = tid * 4 < H;
+  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int start = 0;
+  for (int j = 0; j < cnt; ++j) {
+    const uint32_t id = (uint32_t)(k[j] >> 32);
+    const uint32_t row = (uint32_t)k[j];
+    if (act) acc += *reinterpret_cast<const f32x4*>(de + (int64_t)row * H + 4 * tid);
+    const bool last = j == cnt - 1 || (uint32_t)(k[j + 1] >> 32) != id;
+    if (!last) continue;
+    if (id != 0 && act) {
+      const bool began = start > 0 || prev != id;
+      const bool ends = j < cnt - 1 || next != id;
+      if (began && ends) {
+        f32x4* t = reinterpret_cast<f32x4*>(table + (int64_t)id * H + 4 * tid);
+        *t = *t + acc;
+      } else {
+        *reinterpret_cast<f32x4*>(parts + (c * 2 + (began ? 1 : 0)) * H + 4 * tid) = acc;
+      }
+    }
+    acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    start = j + 1;
+  }
+}
+
+// one workgroup per chunk: the first chunk of a run that crosses into the next chunk adds the run's
+// pieces in chunk order
+__global__ __launch_bounds__(256) void seg_join_kernel(int64_t n, int H, const uint64_t* __restrict__ keys,
+                                                       float* __restrict__ table,
+                                                       const float* __restrict__ parts) {
+  const int64_t c = blockIdx.x, i0 = c * SEG_C;
+  const int64_t iend = min(n, i0 + SEG_C);  // one past the chunk's last position
+  const uint32_t id = seg_id(keys, n, iend - 1);
+  if (id == 0 || seg_id(keys, n, iend) != id) return;  // padding row, or the run ends here
+  // the run began in an earlier chunk: that chunk joins it
+  if (seg_id(keys, n, i0) == id && seg_id(keys, n, i0 - 1) == id) return;
+  const int tid = threadIdx.x;
+  if (tid * 4 >= H) return;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(parts + (c * 2 + 1) * H + 4 * tid);
+  for (int64_t cc = c + 1; cc * SEG_C < n; ++cc) {
+    acc += *reinterpret_cast<const f32x4*>(parts + (cc * 2 + 0) * H + 4 * tid);
+    const int64_t e = min(n, (cc + 1) * SEG_C);
+    if (seg_id(keys, n, e - 1) != id || seg_id(keys, n, e) != id) break;
+  }
+  f32x4* t = reinterpret_cast<f32x4*>(table + (int64_t)id * H + 4 * tid);
+  *t = *t + acc;
+}
+
+size_t table_scatter_sort_bytes(int64_t n) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_keys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                           (unsigned int)n, 0, 64);
+  return bytes;
+}
+
+// workspace (bytes): 2 n keys + the sort's scratch + [nch][2][H] fp32 pieces
+int64_t table_scatter_det_bytes(int64_t n, int H) {
+  const int64_t nch = (n + SEG_C - 1) / SEG_C;
+  return 16 * n + (((int64_t)table_scatter_sort_bytes(n) + 15) & ~15ll) + nch * 2 * H * 4;
+}
+
+mmseq_status table_scatter_det(int64_t n, int H, const int64_t* ids, const float* de, float* table,
+                               void* ws, hipStream_t s) {
+  if (n == 0) return MMSEQ_OK;
+  const int64_t nch = (n + SEG_C - 1) / SEG_C;
+  uint64_t* kin = reinterpret_cast<uint64_t*>(ws);
+  uint64_t* kout = kin + n;
+  size_t bytes = table_scatter_sort_bytes(n);
+  void* tmp = kout + n;
+  float* parts = reinterpret_cast<float*>(reinterpret_cast<char*>(tmp) + ((bytes + 15) & ~size_t(15)));
+  hipLaunchKernelGGL(row_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, ids, kin);
+  if (rocprim::radix_sort_keys(tmp, bytes, (const uint64_t*)kin, kout, (unsigned int)n, 0, 64, s) !=
+      hipSuccess)
+    return mmseq_set_error(MMSEQ_EHIP, "embed_bwd: radix sort failed");
+  hipLaunchKernelGGL(seg_rows_kernel, dim3((unsigned)nch), dim3(256), 0, s, n, H, kout, de, table, parts);
+  hipLaunchKernelGGL(seg_join_kernel, dim3((unsigned)nch), dim3(256), 0, s, n, H, kout, table, parts);
+  return mmseq_check_launch("embed_bwd table scatter");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -616,9 +730,11 @@ extern "C" mmseq_status mmseq_embed_ln_fwd(int P, int Lt, int H, const int64_t* 
 extern "C" int64_t mmseq_embed_ln_bwd_workspace(int P, int Lt, int H) {
   const int64_t rows = (int64_t)P * Lt;
   const int nb = (int)((rows + RPB - 1) / RPB);
-  // de | LN partials + reduction scratch | the column-sum scratch of dpos
+  // de | LN partials + reduction scratch | the column-sum scratch of dpos | the table scatter's
+  // keys, sort scratch and pieces (floats, 16-byte aligned)
   const int64_t cs = Lt > 1 ? mmseq_colsum_workspace(P, (Lt - 1) * H) : 0;
-  return rows * H + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H) + cs;
+  const int64_t head = (rows * H + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H) + cs + 3) & ~3ll;
+  return head + (table_scatter_det_bytes(rows, H) + 3) / 4;
 }
 
 extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* ids,
@@ -629,7 +745,8 @@ extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* 
                                            float* dpos, float* dtype_tab, float* dgamma,
                                            float* dbeta, float* workspace, mmseq_dtype dtype,
                                            const mmseq_dropout* drop, mmseq_stream stream) {
-  MMSEQ_REQUIRE(P >= 0 && Lt > 0 && H > 0 && H <= 1024, "embed_bwd: bad sizes");
+  MMSEQ_REQUIRE(P >= 0 && Lt > 0 && H > 0 && H <= 1024 && H % 4 == 0, "embed_bwd: bad sizes");
+  MMSEQ_REQUIRE((((uintptr_t)workspace) & 15) == 0, "embed_bwd: workspace not 16-byte aligned");
   MMSEQ_REQUIRE(workspace && djoint && dword && dpos, "embed_bwd: null buffer");
   if (P == 0) return MMSEQ_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -639,14 +756,25 @@ extern "C" mmseq_status mmseq_embed_ln_bwd(int P, int Lt, int H, const int64_t* 
   float* ws_ln = workspace + rows * H;
   if (dtype == MMSEQ_F32)
     hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, P, Lt, H, ids, tt,
-                       word, pos, type, gamma, mean, rstd, (const float*)djoint, ld_pair, dword,
-                       dtype_tab, ws_de, ws_ln, make_drop(drop));
+                       word, pos, type, gamma, mean, rstd, (const float*)djoint, ld_pair,
+                       ws_de, ws_ln, make_drop(drop));
   else
     hipLaunchKernelGGL(embed_bwd_kernel<unsigned short>, dim3(nb), dim3(256), 0, s, P, Lt, H, ids,
                        tt, word, pos, type, gamma, mean, rstd, (const unsigned short*)djoint,
-                       ld_pair, dword, dtype_tab, ws_de, ws_ln, make_drop(drop));
+                       ld_pair, ws_de, ws_ln, make_drop(drop));
   mmseq_status st = mmseq_check_launch("embed_ln_bwd");
   if (st) return st;
+  {  // word / token-type tables: fixed-order sums per id (no float atomics)
+    const int64_t cs = Lt > 1 ? mmseq_colsum_workspace(P, (Lt - 1) * H) : 0;
+    const int64_t head = (rows * H + (int64_t)nb * 2 * H + mmseq_reduce_extra(nb, 2 * H) + cs + 3) & ~3ll;
+    void* tws = workspace + head;
+    st = table_scatter_det(rows, H, ids, ws_de, dword, tws, s);
+    if (st) return st;
+    if (tt && dtype_tab) {
+      st = table_scatter_det(rows, H, tt, ws_de, dtype_tab, tws, s);
+      if (st) return st;
+    }
+  }
   // dpos[t] += sum_p de[p][t] for t >= 1 (row 0 = padding_idx): a deterministic column sum over the
   // P pairs of de viewed as [P][Lt * H] (a sequential loop over P per column was latency-bound)
   if (Lt > 1) {

@@ -63,6 +63,10 @@ __global__ __launch_bounds__(256) void pointer_fwd_kernel(int B, int N, int H,
   }
 }
 
+// One workgroup per story b, every sum in a fixed order (no float atomics: the backward is
+// bit-stable run to run): dq / dkey per (t, j), dokey[b][j] summed over t, and the story's
+// partials of dw (tanh_linear.weight) and dw_bias into ws[b][H + 1], which pointer_bwd_reduce
+// sums over the stories in order.
 __global__ __launch_bounds__(256) void pointer_bwd_kernel(int B, int N, int H,
                                                           const float* __restrict__ q,
                                                           const float* __restrict__ key,
@@ -76,43 +80,61 @@ __global__ __launch_bounds__(256) void pointer_bwd_kernel(int B, int N, int H,
                                                           float* __restrict__ dq,
                                                           float* __restrict__ dkey,
                                                           float* __restrict__ dokey,
-                                                          float* __restrict__ dw,
-                                                          float* __restrict__ dwb) {
-  __shared__ float de[MAXN];
-  const int b = blockIdx.x / N, t = blockIdx.x % N;
+                                                          float* __restrict__ ws) {
+  __shared__ float de[MAXN * MAXN];
+  const int b = blockIdx.x;
   const int L = (int)tgt_len[b];
-  if (threadIdx.x < N) {
-    const int j = threadIdx.x;
-    const int tg = (int)target[(int64_t)b * N + t];
-    float g = t < L ? dnll[(int64_t)b * N + t] : 0.f;
-    float sm = expf(logp[((int64_t)b * N + t) * N + j]);
+  for (int e = threadIdx.x; e < N * N; e += 256) {
+    const int t = e / N, j = e - t * N;
+    const int64_t bt = (int64_t)b * N + t;
+    const int tg = (int)target[bt];
+    const float g = t < L ? dnll[bt] : 0.f;
+    const float sm = expf(logp[bt * N + j]);
     // masked entries were overwritten with -1e9 (masked_fill_): no gradient flows through them
-    const bool masked = pointed[((int64_t)b * N + t) * N + j] != 0 || j >= L;
-    de[j] = masked ? 0.f : g * (sm - (j == tg ? 1.f : 0.f));
+    const bool masked = pointed[bt * N + j] != 0 || j >= L;
+    de[e] = masked ? 0.f : g * (sm - (j == tg ? 1.f : 0.f));
   }
   __syncthreads();
+  float* wsb = ws + (int64_t)b * (H + 1);
   if (threadIdx.x == 0) {
     float s = 0.f;
-    for (int j = 0; j < N; ++j) s += de[j];
-    atomicAdd(dwb, s);
+    for (int e = 0; e < N * N; ++e) s += de[e];
+    wsb[H] = s;
   }
-  const float* qr = q + ((int64_t)b * N + t) * H;
   for (int h = threadIdx.x; h < H; h += 256) {
-    float dqh = 0.f, dwh = 0.f;
-    const float wh = w[h], qh = qr[h];
+    const float wh = w[h];
+    float dwh = 0.f;
     for (int j = 0; j < N; ++j) {
-      const int64_t kidx = (((int64_t)b * N + t) * N + j) * H + h;
-      const int64_t oidx = ((int64_t)b * N + j) * H + h;
-      float th = tanhf(qh + key[kidx] + okey[oidx]);
-      float d = de[j] * wh * (1.f - th * th);
-      dkey[kidx] = d;
-      dqh += d;
-      dwh += de[j] * th;
-      atomicAdd(dokey + oidx, d);
+      const float okh = okey[((int64_t)b * N + j) * H + h];
+      float dok = 0.f;
+      for (int t = 0; t < N; ++t) {
+        const int64_t bt = (int64_t)b * N + t;
+        const int64_t kidx = (bt * N + j) * H + h;
+        const float th = tanhf(q[bt * H + h] + key[kidx] + okh);
+        const float dj = de[t * N + j];
+        const float d = dj * wh * (1.f - th * th);
+        dkey[kidx] = d;
+        float* dqp = dq + bt * H + h;  // this thread's own element: summed over j in order
+        *dqp = j == 0 ? d : *dqp + d;
+        dok += d;
+        dwh += dj * th;
+      }
+      dokey[((int64_t)b * N + j) * H + h] += dok;
     }
-    dq[((int64_t)b * N + t) * H + h] = dqh;
-    atomicAdd(dw + h, dwh);
+    wsb[h] = dwh;
   }
+}
+
+// dw[h] += sum_b ws[b][h], dw_bias += sum_b ws[b][H], stories in order
+__global__ __launch_bounds__(256) void pointer_bwd_reduce(int B, int H, const float* __restrict__ ws,
+                                                          float* __restrict__ dw,
+                                                          float* __restrict__ dwb) {
+  const int h = blockIdx.x * 256 + threadIdx.x;
+  if (h > H) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += ws[(int64_t)b * (H + 1) + h];
+  if (h < H) dw[h] += s;
+  else dwb[0] += s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -397,19 +419,27 @@ extern "C" mmseq_status mmseq_pointer_fwd(int B, int N, int H, const float* q, c
   return mmseq_check_launch("pointer_fwd");
 }
 
+extern "C" int64_t mmseq_pointer_bwd_workspace(int B, int N, int H) {
+  (void)N;
+  return (int64_t)B * (H + 1);
+}
+
 extern "C" mmseq_status mmseq_pointer_bwd(int B, int N, int H, const float* q, const float* key,
                                           const float* okey, const float* w, const float* logp,
                                           const uint8_t* pointed, const int64_t* tgt_len, const int64_t* target,
                                           const float* dnll, float* dq, float* dkey, float* dokey,
-                                          float* dw, float* dw_bias, mmseq_stream stream) {
+                                          float* dw, float* dw_bias, float* workspace,
+                                          mmseq_stream stream) {
   MMSEQ_REQUIRE(B >= 0 && N > 0 && N <= MAXN && H > 0, "pointer_bwd: bad sizes");
   MMSEQ_REQUIRE(q && key && okey && w && logp && pointed && tgt_len && target && dnll && dq &&
-                    dkey && dokey && dw && dw_bias,
+                    dkey && dokey && dw && dw_bias && workspace,
                 "pointer_bwd: null buffer");
   if (!B) return MMSEQ_OK;
-  hipLaunchKernelGGL(pointer_bwd_kernel, dim3(B * N), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), B, N, H, q, key, okey, w, logp,
-                     pointed, tgt_len, target, dnll, dq, dkey, dokey, dw, dw_bias);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(pointer_bwd_kernel, dim3(B), dim3(256), 0, s, B, N, H, q, key, okey, w, logp,
+                     pointed, tgt_len, target, dnll, dq, dkey, dokey, workspace);
+  hipLaunchKernelGGL(pointer_bwd_reduce, dim3((H + 1 + 255) / 256), dim3(256), 0, s, B, H, workspace,
+                     dw, dw_bias);
   return mmseq_check_launch("pointer_bwd");
 }
 

@@ -81,6 +81,14 @@ class fp8_forward:
             _FP8["cache"].clear()
 
 
+def _fp8_bwd_done(f8):
+    """End of a layer backward that ran its dgrads on the fp8 MFMA (ctx.f8dg, captured in the
+    forward): when that backward runs after the fp8_forward() context has exited, the transposed
+    weights' fp8 copies it quantised would stay in the cache until another context exits."""
+    if f8 and not _FP8["on"]:
+        _FP8["cache"].clear()
+
+
 def _fp8_weight(st, W):
     key = (W.data_ptr(), tuple(W.shape))
     hit = _FP8["cache"].get(key)
@@ -106,10 +114,13 @@ def _f8_train(x, *Ws):
             and x.is_contiguous() and all(W.shape[0] % 256 == 0 and W.shape[1] % 256 == 0 for W in Ws))
 
 
-def _mx(x):
+def _mx(x, hit=None):
     """The MX-fp8 copy of activation x: the one its producer (a fused LayerNorm) attached, if x has
-    not been modified since, else a quantisation pass (mmseq_quant_mxfp8)."""
-    hit = getattr(x, "_mx", None)
+    not been modified since, else a quantisation pass (mmseq_quant_mxfp8). The attached copy is
+    detached on use (or passed in as `hit`, already detached by the consumer): x itself is often
+    saved for backward, and an attribute would keep the fp8 copy alive with it until then."""
+    if hit is None:
+        hit = x.__dict__.pop("_mx", None)
     if hit is not None and hit[1] == x._version:
         return hit[0]
     return N.quant_mxfp8(x.view(-1, x.shape[-1]))
@@ -125,11 +136,13 @@ def _lin8(st, x, W, bias=None, resid=None, xq=None):
     return out
 
 
-def _ln8(x, gamma, beta, eps, y=None, mean=None, rstd=None):
+def _ln8(x, gamma, beta, eps, y=None, mean=None, rstd=None, attach=False):
     """LayerNorm of x whose output also leaves in MX-fp8 (mmseq_layernorm_fwd_mxfp8); with y the
-    bf16 output too, its MX-fp8 copy attached for the next fp8 GEMM (_mx)."""
+    bf16 output too. attach=True (a layer's output, consumed by the NEXT layer's first GEMM): the
+    MX-fp8 copy rides on y until that consumer's _mx detaches it. Copies the caller uses directly
+    are returned only: never attached to a tensor that goes into save_for_backward."""
     q = N.layernorm_fwd_mxfp8(x.shape[0], x.shape[-1], x, gamma, beta, eps, y=y, mean=mean, rstd=rstd)
-    if y is not None:
+    if y is not None and attach:
         y._mx = (q, y._version)  # valid while y is unmodified (_mx checks the version)
     return q
 
@@ -252,15 +265,20 @@ class BertLayerFn(torch.autograd.Function):
         st = L.store
         H = x.shape[-1]
         d_att, d_o, d_out = drops
+        # the previous layer's MX-fp8 copy of x (fp8_forward): detached here so that saving x for
+        # backward does not keep it alive; the paths that do not read it drop it
+        xmx = x.__dict__.pop("_mx", None)
         Wqkv = st.packed(L.qkv_w, "w")
         bqkv = st.packed(L.qkv_b, "f32").view(-1)
         if Tq is not None and Tq < T:
             return BertLayerFn._forward_rows(ctx, x, key_bias, L, P, T, Tq, heads, eps, drops, save,
                                              Wqkv, bqkv)
         if save and _f8_train(x, Wqkv, st.w(L.o_w), st.w(L.i_w), st.w(L.out_w)):
-            return BertLayerFn._forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv)
+            return BertLayerFn._forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv,
+                                                 xmx)
         f8 = not save and _f8(x, Wqkv) and d_att is None and d_o is None
-        qkv = _lin8(st, x, Wqkv, bias=bqkv) if f8 else _linear(x, Wqkv, bias=bqkv)
+        qkv = _lin8(st, x, Wqkv, bias=bqkv, xq=_mx(x, xmx)) if f8 else _linear(x, Wqkv, bias=bqkv)
+        del xmx
         lse = torch.empty(P, heads, T, device=x.device)
         if f8:  # eval: attention writes the output projection's MX-fp8 operand directly
             oq = N.attn_fwd_mxfp8(P, T, heads, qkv, 3 * H, 0, H, 2 * H, key_bias,
@@ -340,7 +358,7 @@ class BertLayerFn(torch.autograd.Function):
         return y
 
     @staticmethod
-    def _forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv):
+    def _forward_f8_train(ctx, x, key_bias, L, P, T, heads, eps, drops, Wqkv, bqkv, xmx=None):
         """Training forward with QKV / O / FC1 / FC2 on the fp8 MFMA: the bf16 tensors the (bf16)
         backward reads are written by the same producers that write the next GEMM's MX-fp8
         operand (attention O, LayerNorm h1 / y, FC1's GELU output + pre-activation)."""
@@ -349,7 +367,8 @@ class BertLayerFn(torch.autograd.Function):
         R = x.shape[0]
         d_att, d_o, d_out = drops
         qkv = torch.empty(R, 3 * H, device=x.device, dtype=x.dtype)
-        N.gemm_mxfp8_ex(_mx(x), _fp8_weight(st, Wqkv), qkv, bias=bqkv)
+        N.gemm_mxfp8_ex(_mx(x, xmx), _fp8_weight(st, Wqkv), qkv, bias=bqkv)
+        del xmx
         lse = torch.empty(P, heads, T, device=x.device)
         kbits = N.attn_keep_bits(P, T, heads, x.device) if d_att is not None else None
         o = torch.empty_like(x)
@@ -375,7 +394,7 @@ class BertLayerFn(torch.autograd.Function):
         y = torch.empty_like(x)
         m2 = torch.empty_like(m1)
         r2 = torch.empty_like(m1)
-        _ln8(s2, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=y, mean=m2, rstd=r2)
+        _ln8(s2, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=y, mean=m2, rstd=r2, attach=True)
         ctx.save_for_backward(x, key_bias, qkv, o, lse, s1, m1, r1, h1, z, gact, s2, m2, r2)
         ctx.meta = (L, P, T, heads, drops)
         ctx.kbits = kbits
@@ -401,7 +420,7 @@ class BertLayerFn(torch.autograd.Function):
             s2 = _mlp_fwd(st, h1, st.w(L.i_w), st.f32(L.i_b), GELU, st.w(L.out_w), st.f32(L.out_b),
                           h1, _linear)
         y = torch.empty_like(x)
-        _ln8(s2, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=y, mean=m, rstd=r)
+        _ln8(s2, st.f32(L.ln2_w), st.f32(L.ln2_b), eps, y=y, mean=m, rstd=r, attach=True)
         return y
 
     @staticmethod
@@ -473,6 +492,7 @@ class BertLayerFn(torch.autograd.Function):
         st.grad_ready(L.span)
         dx = _dgrad8(dqkv, st, st.wt(L.qkv_w[0]), resid=ds1, dyq=dqkvq) if f8 else \
             _dgrad(dqkv, st.wt(L.qkv_w[0]), resid=ds1)
+        _fp8_bwd_done(f8)
         return dx, None, None, None, None, None, None, None, None, None, None
 
 
@@ -606,6 +626,7 @@ class VitBlockFn(torch.autograd.Function):
         N.layernorm_bwd(R, W, dhn, _rows(W), h, _rows(W), m1, r1, st.f32(L.ln1_w), dh, _rows(W),
                         dx1, _rows(W), st.g(L.ln1_w), st.g(L.ln1_b))
         st.grad_ready(L.span)
+        _fp8_bwd_done(f8)
         return dh, None, None, None, None, None, None, None
 
 

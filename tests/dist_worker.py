@@ -151,15 +151,14 @@ def real(out, rank):
     phase[0] = "finish"
     red.finish()
     torch.cuda.synchronize()
-    # the embedding-table and pointer-head backward kernels accumulate with float atomics, so
-    # two backwards agree to rounding, not bitwise (`nondeterministic`); a bucket issued before
-    # its gradients were final would miss whole contributions (differences at gradient scale)
+    # the backward is bit-stable (fixed-order sums everywhere, `nondeterministic` must be empty),
+    # so every bucket's chunk at issue time must equal the final local gradient bit for bit; a
+    # bucket issued before its gradients were final would miss whole contributions
     bad = []
     for i, lo, hi, snap, _ in snaps:
         ref = local[i][lo:hi]
-        err = float((snap - ref).abs().max())
-        if err > 1e-5 * float(ref.abs().max()) + 1e-12:
-            bad.append((i, lo, hi, err, float(ref.abs().max())))
+        if not torch.equal(snap, ref):
+            bad.append((i, lo, hi, float((snap - ref).abs().max()), float(ref.abs().max())))
     total = sum(len(red.plan[id(s)]["buckets"]) for s in stores)
     res = {"fired_in_backward": in_backward, "buckets": total, "snapshots": len(snaps),
            "early": bad, "loss": float(loss.detach()), "nondeterministic": nondet,

@@ -4,10 +4,9 @@ backwards). Two ranks share the box's one GPU over gloo (tests/dist_worker.py mo
 launched as a child process of this test by torch.distributed.run.
 
 Checked: (1) every bucket's chunk, snapshotted at the instant its all-reduce is issued, equals
-the rank's final local gradient of an unarmed backward of the same story (to 1e-5 of the chunk's
-largest element: the embedding-table and pointer-head backwards add with float atomics, so two
-backwards agree to rounding — measured <= 1e-6 relative — while a bucket issued early would miss
-whole contributions) — no bucket fires before its gradients are final, including the BERSON head
+the rank's final local gradient of an unarmed backward of the same story bit for bit (the backward
+is bit-stable: two unarmed backwards are compared first; a bucket issued early would miss whole
+contributions) — no bucket fires before its gradients are final, including the BERSON head
 store that counts as complete at the inner model's first backward begin (trainer.py
 GradAllReduce._begin); (2) >= 10 buckets are issued during the backward itself, and every
 unit-covered bucket is; (3) the averaged gradients are bitwise equal across ranks and equal
@@ -36,10 +35,9 @@ def test_dp_reducer_real_backward_two_ranks(tmp_path):
     single = torch.load(tmp_path / "single.pt")
     for r, it in enumerate(info):
         print(f"rank {r}: {it['buckets']} buckets, {it['fired_in_backward']} issued during the "
-              f"backward, float-atomic spread {it['nondeterministic']}")
+              f"backward, run-to-run differences {it['nondeterministic']}")
     for r, it in enumerate(info):
-        for i, err, scale in it["nondeterministic"]:  # float-atomic rounding only
-            assert err <= 1e-6 * scale, (r, it["nondeterministic"])
+        assert it["nondeterministic"] == [], (r, it["nondeterministic"])  # bit-stable backward
         assert it["early"] == [], (r, it["early"], it["fired"])  # no chunk changed after it fired
         assert it["snapshots"] == it["buckets"]
         assert it["fired_in_backward"] >= 10, it
@@ -58,7 +56,7 @@ def test_rccl_reducer_world1(tmp_path):
     """The reducer's RCCL branch (ReduceOp.AVG, trainer.py GradAllReduce._fire) executed on the
     box's GPU: backend "nccl" at world size 1 (RCCL refuses two ranks on one GPU), the reducer
     forced on, buckets issued during the real backward and finished; at world 1 the mean is the
-    local gradient (float-atomic rounding aside)."""
+    local gradient bit for bit."""
     port = 29500 + (os.getpid() * 17 + 7) % 2000
     subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                     "--nproc-per-node=1", "--master-addr", "127.0.0.1", "--master-port",
@@ -71,4 +69,4 @@ def test_rccl_reducer_world1(tmp_path):
     assert it["avg_bucket_equal"]
     assert it["armed"] and it["fired_in_backward"] >= 10
     assert it["avg_ops"] == it["fired_in_backward"]  # the RCCL AVG branch, not gloo's SUM + div
-    assert it["max_rel_diff"] <= 1e-5, it
+    assert it["max_rel_diff"] == 0.0, it

@@ -440,6 +440,55 @@ def test_embed_ln_fwd_bwd(dtype):
     assert dw.abs().sum() > 0
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_embed_table_grad_fixed_order(dtype):
+    """The word / token-type table gradients in a fixed order (rows grouped by id, summed in row
+    order; no float atomics): ids 1 and 2 make runs that cross many 64-row chunks of the sorted
+    order, most other ids occur once, id 0 (padding_idx) never gets a gradient, type id 1 does;
+    equal to a float64 index_add and bitwise equal across calls."""
+    P, Lt, Tv, H = 64, 40, 3, 256
+    T = Lt + Tv
+    g = torch.Generator(device="cpu").manual_seed(11)
+    V = 3000
+    ids = torch.randint(3, V, (P, Lt), generator=g)
+    ids[torch.rand(P, Lt, generator=g) < 0.3] = 1
+    ids[torch.rand(P, Lt, generator=g) < 0.2] = 2
+    ids[torch.rand(P, Lt, generator=g) < 0.05] = 0
+    ids = ids.to(DEV)
+    tt = (torch.rand(P, Lt, generator=g) < 0.5).long().to(DEV)
+    word = torch.randn(V, H, generator=g).to(DEV)
+    pos = torch.randn(Lt, H, generator=g).to(DEV)
+    typ = torch.randn(2, H, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(H, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(H, generator=g)).to(DEV)
+    joint = torch.zeros(P, T, H, device=DEV, dtype=dtype)
+    mean = torch.empty(P * Lt, device=DEV)
+    rstd = torch.empty(P * Lt, device=DEV)
+    nat.embed_ln_fwd(P, Lt, H, ids, tt, word, pos, typ, gam, bet, 1e-12, joint, T * H, mean, rstd)
+    dj = torch.randn(P, T, H, generator=g).to(DEV, dtype)
+    runs = []
+    for _ in range(2):
+        dw, dp, dty = torch.zeros_like(word), torch.zeros_like(pos), torch.zeros_like(typ)
+        dg, db = torch.zeros_like(gam), torch.zeros_like(bet)
+        nat.embed_ln_bwd(P, Lt, H, ids, tt, word, pos, typ, gam, mean, rstd, dj, T * H, dw, dp, dty,
+                         dg, db)
+        runs.append((dw, dty))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+    w_, t_ = word.double().requires_grad_(True), typ.double().requires_grad_(True)
+    posid = torch.arange(Lt, device=DEV)[None].expand(P, Lt)
+    e = (torch.nn.functional.embedding(ids, w_, padding_idx=0)
+         + torch.nn.functional.embedding(posid, pos.double(), padding_idx=0)
+         + torch.nn.functional.embedding(tt, t_, padding_idx=0))
+    ref = torch.nn.functional.layer_norm(e, (H,), gam.double(), bet.double(), 1e-12)
+    rw, rt = torch.autograd.grad(ref, (w_, t_), dj[:, :Lt].double())
+    dw, dty = runs[0]
+    assert not dw[0].any() and not dty[0].any()  # padding_idx rows
+    tol = dict(rtol=1e-5, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(dw.double(), rw, **tol)
+    torch.testing.assert_close(dty.double(), rt, **tol)
+    assert dw[1].abs().sum() > 0 and dty[1].abs().sum() > 0
+
+
 @pytest.mark.parametrize("dtype,W", [(torch.float32, 64), (torch.bfloat16, 64), (torch.bfloat16, 768),
                                      (torch.bfloat16, 1024)])
 def test_vit_im2col_embed_fwd_bwd(dtype, W):

@@ -21,6 +21,8 @@ from golden_util import GOLDEN
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+# relative gradient difference, text-rows vs full-size last layer (bf16, real_config5_l2 shape)
+ROWS_GRAD_BOUND = 1e-5
 
 
 def _qkv(P, T, heads, seed):
@@ -126,17 +128,18 @@ def test_text_rows_last_layer_equals_full_layer_in_training():
     print(f"attention dropout only: loss full {l0!r} text rows {l1!r}; gradient rel diff to a second "
           f"full run {d_self:.3e}, to the text-rows run {d_rows:.3e}")
     assert l1 == l0 == l0b
-    # the pointer head and embedding backwards accumulate with float atomics, so two
-    # full-size backwards already differ at bf16-rounding level; the text-rows run may differ from
-    # the full one by no more than that (plus the last layer's fp32 split-K regrouping)
-    assert d_rows < max(1e-5, 3 * d_self), (d_rows, d_self)
+    # the backward is bit-stable (fixed-order table and pointer-head sums, test_determinism_gpu);
+    # the text-rows run differs from the full one only by the last layer's fp32 weight-gradient
+    # regrouping (its split-K slabs cover fewer rows)
+    assert d_self == 0.0, d_self
+    assert d_rows <= ROWS_GRAD_BOUND, d_rows
     (l0, g0), (l1, g1), (l2, g2) = run(False), run(True), run(True)
     cos = float(g1 @ g0 / (g1.norm() * g0.norm()))
     print(f"all dropout: loss full {l0!r} text rows {l1!r}; gradient cosine {cos:.5f}")
     # a different draw of two of the layer's masks: as different from the full run as any other
     # dropout sample (this 4-layer model's loss moves ~1 % between samples), so only repeatability
     # and finiteness are asserted here
-    assert l2 == l1 and float((g2 - g1).norm() / g1.norm()) < max(1e-5, 3 * d_self)
+    assert l2 == l1 and torch.equal(g2, g1)
     assert torch.isfinite(g1).all() and abs(l1 - l0) < 0.1 * abs(l0)
     m.eval()
     orders = []
