@@ -54,6 +54,16 @@ def story_flops(Pst, Lt, Tv, H, Lj, W, Lv, patch, E, ff=4):
     return Pst * (vit + visn + joint) + head
 
 
+def rows_layer_saving(Pst, Lt, Tv, H):
+    """Forward FLOPs per story the text-rows last joint layer (kernels.ROWS) does not
+    execute: the full layer 2 (12 T H^2 + 2 T^2 H) minus QKV over all T rows, attention for the
+    Lt text queries against T keys, and the output projection + FFN on the Lt rows."""
+    T = Lt + Tv
+    full = 2 * (12 * T * H * H + 2 * T * T * H)
+    rows = 2 * (3 * T * H * H + 9 * Lt * H * H + 2 * Lt * T * H)
+    return Pst * (full - rows)
+
+
 def synthetic_story(idx, Nst, per_seq, vocab, res, seed):
     """Story `idx` of the synthetic dataset: each step = <s>(0) + k ids
     ~ U[3, vocab) + </s>(2), labels = argsort(randperm(N)), images ~ N(0, 1). A pure function of
@@ -470,6 +480,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timer.on = True
+    if reducer is not None:
+        reducer.timing = True
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
@@ -480,6 +492,19 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     timer.on = False
+    ar_stats = None
+    if reducer is not None:
+        reducer.timing = False
+        mine = reducer.timing_summary() or {}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        ar_stats = {"buckets_per_step": mine.get("buckets"),
+                    "issued_during_backward": mine.get("issued_in_backward"),
+                    "exposed_ms_per_step_by_rank": [e.get("exposed_ms_mean") for e in every],
+                    "exposed_ms_max_by_rank": [e.get("exposed_ms_max") for e in every],
+                    "definition": "GPU time the compute stream waits inside GradAllReduce.finish() "
+                                  "after the last backward kernel (HIP events around the waits), "
+                                  "mean over the timed steps"}
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -546,6 +571,8 @@ def main():
     Lt = 2 * per
     fwd = story_flops(Pst, Lt, Tv, J["hidden_size"], J["num_hidden_layers"], V["width"],
                       V["layers"], V["patch"], V["embed"])
+    # FLOPs actually executed: the text-rows last joint layer skips its visual rows' work
+    fwd_exec = fwd - (rows_layer_saving(Pst, Lt, Tv, J["hidden_size"]) if K.ROWS["on"] else 0)
     stories = args.batch * args.steps * world
     steps_s = args.steps * world / dt
     out = {
@@ -571,8 +598,13 @@ def main():
         "stories_per_s": stories / dt,
         "model_tflops": stories / dt * 3 * fwd / 1e12,
         "model_flops_util": stories / dt * 3 * fwd / 1e12 / PEAK_BF16_TFLOPS,
+        "executed_flops_util": stories / dt * 3 * fwd_exec / 1e12 / PEAK_BF16_TFLOPS,
+        "flops_note": "model FLOPs = the reference's computation (SURVEY 8d); executed = without the "
+                      "last joint layer's visual rows, which the text-rows layer does not compute",
         "loss": float(loss.item()) if loss is not None else None,
     }
+    if ar_stats is not None:
+        out["allreduce"] = ar_stats
     _mpk, _ = measured_peak()
     if _mpk:  # stories/s x (fwd+bwd FLOP/story) / measured peak
         out["model_flops_util_of_measured_peak"] = stories / dt * 3 * fwd / 1e12 / _mpk
@@ -583,6 +615,7 @@ def main():
                           "stories_per_call": fm,
                           "tflops": fst * fwd / 1e12,
                           "mfma_frac": fst * fwd / 1e12 / PEAK_BF16_TFLOPS,
+                          "mfma_frac_executed": fst * fwd_exec / 1e12 / PEAK_BF16_TFLOPS,
                           "mfma_frac_of_measured_peak": (fst * fwd / 1e12 / mpk) if mpk else None,
                           "mode": "eval (no dropout), torch.no_grad, full model forward incl. "
                                   "BERSON head + loss; ViT + joint encoder are >99.9% of FLOPs"}

@@ -211,6 +211,11 @@ class GradAllReduce:
     def __init__(self, stores, bucket_mb=64, units=None, begin_units=(), group=None, force=False):
         self.stores = list(stores)
         self.force = bool(force)
+        # diagnostics (bench.py at N > 1): per finish(), the buckets issued during the backward
+        # and the exposed all-reduce time = GPU time the compute stream waits in finish() after
+        # the last backward kernel (events on the compute stream around the waits)
+        self.timing = False
+        self.records = []
         self.cap = max(1, int(bucket_mb * (1 << 20)) // 4)
         self.group = group
         self.armed = False
@@ -316,15 +321,34 @@ class GradAllReduce:
             return
         if not self.armed:
             self.arm(True)
+        in_backward = len(self.works)
+        e0 = None
+        if self.timing and torch.cuda.is_available() and self.stores[0].grad.is_cuda:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         for s in self.stores:
             for j in range(len(self.plan[id(s)]["buckets"])):
                 self._fire(s, j)
+        total = len(self.works)
         for w, chunk, avg in self.works:
             w.wait()
             if not avg:
                 chunk.div_(world)
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.records.append((e0, e1, total, in_backward))
         self.works = []
         self.armed = False
+
+    def timing_summary(self):
+        """Mean exposed all-reduce ms per finish() and the bucket counts (after a synchronize)."""
+        if not self.records:
+            return None
+        ms = [a.elapsed_time(b) for a, b, _, _ in self.records]
+        return {"exposed_ms_mean": sum(ms) / len(ms), "exposed_ms_max": max(ms),
+                "buckets": self.records[-1][2], "issued_in_backward": self.records[-1][3],
+                "steps": len(ms)}
 
     __call__ = finish
 
