@@ -72,7 +72,8 @@ const char* mmseq_version(void);
  *     128 x 128 double-buffer otherwise), MMSEQ_GEMM_DB128 (128 x 128 double-buffer only),
  *     MMSEQ_GEMM_RING128 (128 x 128 four-slot ring only), MMSEQ_GEMM_BIG_ALWAYS (256 x 256
  *     NT for every eligible NT problem), MMSEQ_GEMM_BIG_256x128 (256 x 128 NT, two blocks/CU),
- *     MMSEQ_GEMM_GENERIC (register-staged kernel only).
+ *     MMSEQ_GEMM_PINGPONG (bf16 NT: two independent 4-wave groups per CU on 256 x 128 tiles, one
+ *     group's epilogue beside the other's main loop), MMSEQ_GEMM_GENERIC (register-staged only).
  *   workspace: caller-owned, 16-byte aligned device scratch for fp32 split-K partial slabs of
  *     this call (NULL / 0 bytes = no split-K). Wgrad-shaped problems (few output tiles, long
  *     K) split K across workgroups and reduce the slabs in a fixed order (bitwise reproducible).
@@ -81,7 +82,7 @@ const char* mmseq_version(void);
  * ------------------------------------------------------------------------------------------ */
 typedef enum {
   MMSEQ_GEMM_GENERIC = 0, MMSEQ_GEMM_AUTO = 1, MMSEQ_GEMM_DB128 = 2, MMSEQ_GEMM_RING128 = 3,
-  MMSEQ_GEMM_BIG_ALWAYS = 4, MMSEQ_GEMM_BIG_256x128 = 5
+  MMSEQ_GEMM_BIG_ALWAYS = 4, MMSEQ_GEMM_BIG_256x128 = 5, MMSEQ_GEMM_PINGPONG = 6
 } mmseq_gemm_variant;
 
 mmseq_status mmseq_gemm(int trans, int M, int N, int K, int batch,

@@ -54,10 +54,10 @@ struct GemmSel {
 };
 
 static bool make_sel(int variant, GemmSel* s) {
-  if (variant < 0 || variant > 5) return false;
+  if (variant < 0 || variant > 6) return false;
   s->disable_fast = variant == 0;
-  s->big = variant == 1 ? 1 : ((variant == 4 || variant == 5) ? 2 : 0);
-  s->nt_variant = variant == 5 ? 1 : 0;
+  s->big = variant == 1 ? 1 : ((variant >= 4) ? 2 : 0);
+  s->nt_variant = variant == 5 ? 1 : (variant == 6 ? 2 : 0);
   s->ring = variant == 3;
   s->nt_delay = 0;
   s->num_cu = device_cus();

@@ -1046,6 +1046,290 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2b_kernel(GemmArgs a, int tile
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong NT kernel (bf16 forward / dgrad, every bf16 epilogue). One 512-thread workgroup per CU
+// holds two independent 4-wave groups; each runs its own persistent sequence of 256 x 128 tiles
+// through its own 3-slot LDS-DMA ring (BK = 32: A [256][32] + B [128][32] = 24 KB per slot). The
+// groups share only the workgroup barrier: every barrier interval is one step of each group's
+// static program, and group 1's program starts an odd number of intervals after group 0's, so
+//  * in the main loop one group reads its fragments and issues its DMA ("load") while the other
+//    runs its 32 MFMAs per wave ("compute"), the roles swapping every interval, and
+//  * a group's epilogue (E intervals, its stores spread over them at ~16 B / cycle per CU, the
+//    per-CU store rate) runs beside the other group's main loop instead of idling the CU's MFMA
+//    pipes (the 8-wave kernel stops every MFMA pipe of the CU for its epilogue bursts).
+// Per group: waves 2 x 2 of 128 x 64 outputs (8 x 4 MFMA 16x16 tiles, the fragment maps and the
+// 16-byte epilogue lanes of the 256 x 256 kernel), images as gemm_nt_2b_kernel's (64-B rows, 16-B
+// chunk c of row r at c ^ (((r >> 3) & 1) << 1)). Epilogue loads and stores are buffer operations
+// on per-tile descriptors: rows past M fall outside the range and columns past N get an
+// out-of-range offset, so every call issues exactly its loads and stores and the counted vmcnt
+// waits (DMA, epilogue operand loads) stay exact. Preconditions as mmseq_gemm256_nt (K % 128 == 0).
+// ---------------------------------------------------------------------------------------------
+constexpr int PP_STAGE = 256 * 32 + 128 * 32;  // elements per ring slot (24 KB)
+
+template <int ACT, bool BWD, bool XIN, bool AUX>
+struct PPCfg {
+  static constexpr int E = ACT < 0 ? 2 : ((AUX || BWD) ? 16 : 8);  // epilogue intervals (even)
+  static constexpr int CPI = ACT < 0 ? 0 : 16 / E;                // 8-output calls per interval
+  static constexpr int NL = ACT >= 0 && XIN ? 1 : 0;              // operand loads per call
+  static constexpr int NS = ACT < 0 ? 0 : (AUX ? 2 : 1);          // stores per call
+  static constexpr int EPO = (ACT < 0 ? 0 : 16) * (NL + NS);      // epilogue VMEM ops per tile
+};
+
+// vmcnt(N) with a compile-time N (N <= 63)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int ACT, bool BWD, bool XIN, bool AUX>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a, int tiles_n, int ntiles, int) {
+  typedef PPCfg<ACT, BWD, XIN, AUX> Cf;
+  constexpr int E = Cf::E, CPI = Cf::CPI, NL = Cf::NL, NS = Cf::NS, EPO = Cf::EPO;
+  static_assert(E % 2 == 0 && 6 + EPO <= 63, "epilogue schedule");
+  __shared__ __attribute__((aligned(16))) unsigned short
+      smem[2 * 3 * PP_STAGE + 2 * 2 * 256 + (BWD ? 4 * DT_N : 0)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, w = wave & 3;
+  const int wr = w >> 1, wc = w & 1;
+  unsigned short* const ring = smem + grp * 3 * PP_STAGE;
+  float MMSEQ_LDS* dtab = (float MMSEQ_LDS*)(smem + 2 * 3 * PP_STAGE + 2 * 2 * 256);
+  if (BWD) dtab_fill<ACT>(dtab);
+  __syncthreads();  // dtab visible; both groups pass it once
+  const int G = gridDim.x;
+  const int item = xcd_item(blockIdx.x, G);
+  const int stride = 2 * G;
+  const int first = 2 * item + grp;
+  const int my_tiles = first < ntiles ? (ntiles - 1 - first) / stride + 1 : 0;
+  const int n0t = 2 * item < ntiles ? (ntiles - 1 - 2 * item) / stride + 1 : 0;
+  const int n1t = 2 * item + 1 < ntiles ? (ntiles - 2 - 2 * item) / stride + 1 : 0;
+  const int nk = a.K >> 5;
+  const int S = 2 * nk + E;
+  const int OFF = (S >> 1) | 1;  // odd: the groups' load / compute roles alternate
+  const int total = max(n0t * S, n1t > 0 ? OFF + n1t * S : 0);
+  if (total == 0) return;
+
+  const uint8_t* Ab = reinterpret_cast<const uint8_t*>(a.A);
+  const uint8_t* Bb = reinterpret_cast<const uint8_t*>(a.B);
+  const int64_t lda_b = 2 * a.lda, ldb_b = 2 * a.ldb;
+  // DMA piece = 16 rows x 64 B: lane -> row lane >> 2, 16-B chunk (lane & 3) ^ swizzle
+  const int psw = ((lane >> 5) & 1) << 1;
+  const uint32_t offA = (uint32_t)((lane >> 2) * lda_b + (((lane & 3) ^ psw) << 4));
+  const uint32_t offB = (uint32_t)((lane >> 2) * ldb_b + (((lane & 3) ^ psw) << 4));
+  auto tile_desc = [&](int tile, rsrc_t& ra, rsrc_t& rb, int& m0, int& n0) {
+    if (tile < ntiles) {
+      int tm, tn;
+      tile_mn(tile, tiles_n, ntiles, tm, tn);
+      m0 = tm * 256;
+      n0 = tn * 128;
+      ra = make_rsrc(Ab + (int64_t)m0 * lda_b, (int64_t)(a.M - m0 - 1) * lda_b + 2 * a.K);
+      rb = make_rsrc(Bb + (int64_t)n0 * ldb_b, (int64_t)(a.N - n0 - 1) * ldb_b + 2 * a.K);
+    } else {
+      ra = rb = make_rsrc(Ab, 0);
+      m0 = n0 = 0;
+    }
+  };
+  // k-step kk (of the tile whose A / B descriptors are given) into ring slot `slot`: 24 pieces,
+  // wave w issues pieces w, w + 4, .., w + 20 (A pieces 0-15, B pieces 16-23)
+  auto stage = [&](const rsrc_t& ra, const rsrc_t& rb, int kk, int slot) {
+    unsigned short* st = ring + slot * PP_STAGE;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int pc = w + 4 * e;
+      if (pc < 16)
+        dma16(ra, st + pc * 512, offA + (uint32_t)(pc * 16 * lda_b + kk * 64));
+      else
+        dma16(rb, st + 256 * 32 + (pc - 16) * 512, offB + (uint32_t)((pc - 16) * 16 * ldb_b + kk * 64));
+    }
+  };
+  // fragment offsets (elements within a slot), as gemm_nt_2b_kernel
+  const int l15 = lane & 15, g = lane >> 4, ii = lane & 15;
+  const int hA = ((l15 >> 3) & 1) << 1;
+  const int aoff = (wr * 128 + l15) * 32 + ((g ^ hA) << 3);
+  const int rB = 8 * (l15 >> 2) + (l15 & 3);
+  const int hB = ((rB >> 3) & 1) << 1;
+  const int boff = 256 * 32 + (wc * 64 + rB) * 32 + ((g ^ hB) << 3);
+
+  int tile = first;
+  rsrc_t rAc, rBc, rAn, rBn;
+  int m0, n0, m0n, n0n;
+  tile_desc(tile, rAc, rBc, m0, n0);
+  tile_desc(tile + stride, rAn, rBn, m0n, n0n);
+  // prologue: k-steps 0 and 1 of the group's first tile (zero-size loads if it has none)
+  stage(rAc, rBc, 0, 0);
+  stage(rAc, rBc, 1, 1);
+  vm_wait<6>();
+  __builtin_amdgcn_s_barrier();
+  int t = 0;  // intervals of this group's program done
+  if (grp) {
+    for (; t < OFF; ++t) __builtin_amdgcn_s_barrier();
+  }
+  const rsrc_t rBias = make_rsrc(a.bias, a.bias ? (int64_t)a.N * 4 : 0);
+  f32x4 acc[8][4];
+  bf16x8_t fa[8], fb[4];
+  for (int it = 0; it < my_tiles; ++it) {
+    float* sbias = reinterpret_cast<float*>(smem + 2 * 3 * PP_STAGE + (grp * 2 + (it & 1)) * 256);
+    if (ACT >= 0 && w == 0 && lane < 32)  // the tile's 128 bias values (read in its epilogue)
+      dma16(rBias, reinterpret_cast<unsigned short*>(sbias), (uint32_t)(n0 * 4) + (uint32_t)lane * 16u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int base = (int)(((int64_t)it * nk) % 3);  // ring slot of the tile's k-step 0
+    for (int k = 0; k < nk; ++k) {
+      // ---- load(k): fragments of k-step k, DMA of k-step k + 2 (the next tile's 0 / 1 at the end)
+      const unsigned short* st = ring + ((base + k) % 3) * PP_STAGE;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fa[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(st + aoff + i * 16 * 32));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(
+                                                 st + boff + (4 * (j & 1) + 32 * (j >> 1)) * 32));
+      if (k + 2 < nk) stage(rAc, rBc, k + 2, (base + k + 2) % 3);
+      else stage(rAn, rBn, k + 2 - nk, (base + k + 2) % 3);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // ---- compute(k)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // k-step k + 1 landed (its DMA is older than k + 2's; for k + 1 == 1 also older than the
+      // previous tile's epilogue operations and this tile's bias DMA)
+      if (k + 1 < nk) {
+        if (k == 0 && it > 0) vm_wait<6 + EPO>();
+        else vm_wait<6>();
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    t += 2 * nk;
+    // ---- epilogue: E intervals of CPI calls each, beside the other group's main loop
+    if (ACT >= 0) {
+      const float* sbr = sbias;  // written by wave 0's DMA, retired by the k = 1 wait + barrier
+      const int64_t rows_left = (int64_t)a.M - m0;
+      const rsrc_t rC = make_rsrc(reinterpret_cast<const uint8_t*>(a.C) + (int64_t)m0 * a.ldc * 2,
+                                  (rows_left - 1) * a.ldc * 2 + (int64_t)a.N * 2);
+      const rsrc_t rX = make_rsrc(AUX ? reinterpret_cast<const uint8_t*>(a.aux) + (int64_t)m0 * a.ldc * 2 : nullptr,
+                                  AUX ? (rows_left - 1) * a.ldc * 2 + (int64_t)a.N * 2 : 0);
+      const bool resid = XIN && !BWD && a.resid != nullptr;
+      const int64_t ldi = BWD ? a.ldc : (resid ? a.ldr : a.ldc);  // operand row stride
+      const uint8_t* ibase = BWD ? reinterpret_cast<const uint8_t*>(a.dact)
+                                 : (resid ? reinterpret_cast<const uint8_t*>(a.resid)
+                                          : reinterpret_cast<const uint8_t*>(a.C));
+      const rsrc_t rI = make_rsrc(XIN ? ibase + (int64_t)m0 * ldi * 2 : nullptr,
+                                  XIN ? (rows_left - 1) * ldi * 2 + (int64_t)a.N * 2 : 0);
+      auto call_off = [&](int call, int64_t ld) -> uint32_t {
+        const int i = call >> 1, tt = call & 1;
+        const int r = wr * 128 + i * 16 + ii;
+        const int n = n0 + wc * 64 + 32 * tt + 8 * g;
+        return n < a.N ? (uint32_t)(((int64_t)r * ld + n) * 2) : 0x80000000u;
+      };
+      typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+      i32x4_t in[2][CPI > 0 ? CPI : 1];
+      if (NL) {  // batch 0's operands (older than nothing we wait for before consuming them)
+#pragma unroll
+        for (int q = 0; q < CPI; ++q)
+          in[0][q] = __builtin_amdgcn_raw_buffer_load_b128(rI, call_off(q, ldi), 0, 0);
+      }
+#pragma unroll
+      for (int c = 0; c < E; ++c) {
+        if (NL && c + 1 < E) {
+#pragma unroll
+          for (int q = 0; q < CPI; ++q)
+            in[(c + 1) & 1][q] = __builtin_amdgcn_raw_buffer_load_b128(rI, call_off((c + 1) * CPI + q, ldi), 0, 0);
+        }
+        if (NL) {  // batch c's operands: younger ops = batch c + 1's loads + batch c - 1's stores
+          if (c == 0) vm_wait<(E > 1 ? NL * CPI : 0)>();
+          else if (c + 1 < E) vm_wait<NL * CPI + NS * CPI>();
+          else vm_wait<NS * CPI>();
+          asm volatile("" ::"v"(in[c & 1][0]));
+        }
+#pragma unroll
+        for (int q = 0; q < CPI; ++q) {
+          const int call = c * CPI + q;
+          const int i = call >> 1, tt = call & 1;
+          const f32x4 lo = acc[i][2 * tt], hi = acc[i][2 * tt + 1];
+          const int cn = wc * 64 + 32 * tt + 8 * g;  // column within the tile
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(sbr + cn);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(sbr + cn + 4);
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = fmaf(lo[r], a.alpha, b0[r]);
+            v[4 + r] = fmaf(hi[r], a.alpha, b1[r]);
+          }
+          u16x8 xin = (u16x8){0, 0, 0, 0, 0, 0, 0, 0};
+          if (NL) xin = __builtin_bit_cast(u16x8, in[c & 1][q]);
+          if (BWD) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] *= dtab[dtab_index(xin[r])];
+          } else if (ACT) {
+            if (AUX) {
+              u16x8 z;
+#pragma unroll
+              for (int r = 0; r < 8; ++r) z[r] = f2bf(v[r]);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, z), rX, call_off(call, a.ldc), 0, 0);
+            }
+            if (ACT == MMSEQ_ACT_GELU_ERF) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
+            }
+          }
+          if (a.drop.thr) {
+            const int m = m0 + wr * 128 + i * 16 + ii;
+            float dm[8];
+            drop_mul_pairs<4>(a.drop, (uint64_t)m * a.N + (n0 + cn), dm);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] *= dm[r];
+          }
+          if (XIN && !BWD) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] += bf2f(xin[r]);
+          }
+          u16x8 o;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = f2bf(v[r]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, o), rC, call_off(call, a.ldc), 0, 0);
+        }
+        // last interval: the next tile's k-step 0 landed (its DMA precedes k-step 1's and every
+        // epilogue operation)
+        if (c == E - 1) vm_wait<6 + EPO>();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+      for (int c = 0; c < E; ++c) {
+        if (c == E - 1) vm_wait<6>();
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    t += E;
+    tile += stride;
+    rAc = rAn;
+    rBc = rBn;
+    m0 = m0n;
+    n0 = n0n;
+    tile_desc(tile + stride, rAn, rBn, m0n, n0n);
+  }
+  for (; t < total; ++t) __builtin_amdgcn_s_barrier();  // both groups pass 1 + total barriers
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
 }  // namespace
 
 bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t s, hipError_t* err,
@@ -1076,6 +1360,36 @@ bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t 
       if (bwd) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, true, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);        \
       else if (xin) hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, true>), GRID, BLOCK, 0, s, a, tn, ntiles, delay); \
       else hipLaunchKernelGGL((KERNEL<MMSEQ_ACT_QUICKGELU, false, false>), GRID, BLOCK, 0, s, a, tn, ntiles, delay);         \
+  }
+  if (variant == 2) {  // ping-pong: two 4-wave groups of 256 x 128 tiles per 512-thread block
+    const int tn = (a.N + 127) / 128;
+    const int ntiles = ((a.M + 255) / 256) * tn;
+    const int grid = (ntiles + 1) / 2 < num_cu ? (ntiles + 1) / 2 : num_cu;
+    const bool aux = a.aux != nullptr;
+    const dim3 GR(grid), BL(512);
+#define PP(ACT_, BWD_, XIN_, AUX_) \
+    hipLaunchKernelGGL((gemm_pp_kernel<ACT_, BWD_, XIN_, AUX_>), GR, BL, 0, s, a, tn, ntiles, 0)
+    switch (a.act) {
+      case 0:
+        if (noepi) PP(-1, false, false, false);
+        else if (xin) PP(0, false, true, false);
+        else PP(0, false, false, false);
+        break;
+      case MMSEQ_ACT_GELU_ERF:
+        if (bwd) PP(MMSEQ_ACT_GELU_ERF, true, true, false);
+        else if (xin) { if (aux) PP(MMSEQ_ACT_GELU_ERF, false, true, true); else PP(MMSEQ_ACT_GELU_ERF, false, true, false); }
+        else if (aux) PP(MMSEQ_ACT_GELU_ERF, false, false, true);
+        else PP(MMSEQ_ACT_GELU_ERF, false, false, false);
+        break;
+      default:
+        if (bwd) PP(MMSEQ_ACT_QUICKGELU, true, true, false);
+        else if (xin) { if (aux) PP(MMSEQ_ACT_QUICKGELU, false, true, true); else PP(MMSEQ_ACT_QUICKGELU, false, true, false); }
+        else if (aux) PP(MMSEQ_ACT_QUICKGELU, false, false, true);
+        else PP(MMSEQ_ACT_QUICKGELU, false, false, false);
+    }
+#undef PP
+    *err = hipGetLastError();
+    return true;
   }
   if (variant == 1 && a.K % 32 == 0) {  // two 256 x 128 blocks per CU
     const int tn = (a.N + 127) / 128;

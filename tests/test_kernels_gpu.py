@@ -537,7 +537,7 @@ def test_vit_im2col_embed_fwd_bwd(dtype, W):
                                     (2048, 2304, 128), (164160 // 8, 768, 3072)])
 @pytest.mark.parametrize("epi", ["plain", "gelu_aux", "qgelu_aux", "drop_resid", "dgelu", "dqgelu",
                                  "accum"])
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [4, 5, 6])
 def test_gemm256_persistent(M, Nn, K, epi, variant):
     """Persistent 256x256 NT kernel (mode 4 forces it) vs the fp32 reference, and bit-for-bit
     the same dropout mask as the 128x128 path (mode 2) on the same descriptor."""
@@ -587,6 +587,39 @@ def test_gemm256_persistent(M, Nn, K, epi, variant):
         m4 = outs[0][0] == resid
         m2 = outs[1][0] == resid
         assert (m4 != m2).float().mean().item() < 1e-4
+
+
+@pytest.mark.parametrize("M,Nn,K", [(33000 + 77, 1024, 256), (256 * 3 + 5, 768, 768),
+                                    (2048, 2304, 128), (70001, 768, 384), (4096, 3072, 768)])
+@pytest.mark.parametrize("epi", ["plain", "gelu_aux", "qgelu_aux", "gelu", "drop_resid", "resid",
+                                 "drop", "dgelu", "dqgelu", "accum"])
+def test_gemm_pingpong_equals_8wave(M, Nn, K, epi):
+    """The ping-pong NT kernel (MMSEQ_GEMM_PINGPONG: two 4-wave groups on 256 x 128 tiles) runs
+    the same 16x16x32 MFMA sequence per output as the 8-wave 256 x 256 kernel and the same
+    epilogue math: outputs (and the GELU pre-activation) bit for bit equal, edge tiles included."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + Nn + K)
+    A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(Nn, K, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(Nn, generator=g).to(DEV)
+    resid = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    z_in = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    c0 = torch.randn(M, Nn, generator=g).to(DEV, torch.bfloat16)
+    drop = nat.drop(0.1, 77, 1234) if epi.startswith("drop") else None
+    act = {"gelu_aux": 1, "qgelu_aux": 2, "gelu": 1, "dgelu": 1, "dqgelu": 2}.get(epi, 0)
+    outs = []
+    for mode in (6, 4):
+        nat.gemm_set_fast(mode)
+        C = c0.clone()
+        aux = torch.full_like(C, 3.0) if epi.endswith("aux") else None
+        nat.gemm(A, W, C, M, Nn, K, bias=bias if epi not in ("plain", "accum", "dgelu", "dqgelu") else None,
+                 act=act, aux=aux, dact=z_in if epi in ("dgelu", "dqgelu") else None,
+                 resid=resid if epi.endswith("resid") else None, accumulate=epi == "accum", drop=drop)
+        outs.append((C, aux))
+    nat.gemm_set_fast(1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]), float((outs[0][0].float() - outs[1][0].float()).abs().max())
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("trans,M,N,K", [(1, 1, 768, 38400), (1, 768, 768, 38400), (1, 130, 96, 5000),
