@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
     if (a.drop.thr) {  // the normaliser l keeps the undropped probabilities (dropout after softmax)
-      const uint64_t rowi = (((uint64_t)p * a.heads + h) * T + (q0 + i)) * (uint64_t)((T + 1) & ~1) + k0;
+      const uint64_t rowi = (((uint64_t)p * a.heads + h) * T + (q0 + i)) * (uint64_t)((T + 3) & ~3) + k0;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnArgs a) {
         int qi = qs * 16 + 4 * g + r;
         float pv = __expf(s[qs][r] * a.scale + kbias - sL[qi]);
         const float mul = drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + qb0 + qi) *
-                                               (uint64_t)((T + 1) & ~1) + mykey);
+                                               (uint64_t)((T + 3) & ~3) + mykey);
         s[qs][r] = pv * mul;
         dp[qs][r] = pv * (dp[qs][r] * mul - sD[qi]);
       }
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         float pv = __expf(s[kb][r] * a.scale + sBias[kb * 16 + 4 * g + r] - L);
         const float mul =
-            drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + myq) * (uint64_t)((T + 1) & ~1) + k0 +
+            drop_mul(a.drop, (((uint64_t)p * a.heads + h) * T + myq) * (uint64_t)((T + 3) & ~3) + k0 +
                                  kb * 16 + 4 * g + r);
         dp[kb][r] = pv * (dp[kb][r] * mul - D);
       }
@@ -514,8 +514,9 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnArgs a) {
 // c ^ (((r >> 1) & 3) << 1): conflict-free for BOTH the ds_read_b128 row-fragment reads
 // (lane groups of the 16x16x32 operand) and the ds_read_b64_tr_b16 transposed reads, so one image
 // serves S / dP (rows) and dV / dK / dQ (columns). The swizzle is applied to the DMA source.
-// Dropout element index: ((p * heads + h) * T + q) * Tp2 + key, Tp2 = T rounded up to even, so
-// the keys 4g + {0,1} and 4g + {2,3} of a lane share one hash in the forward and dQ kernels.
+// Dropout element index: ((p * heads + h) * T + q) * Tp4 + key, Tp4 = T rounded up to a multiple of
+// 4, so the four keys 4g .. 4g + 3 of a lane are one hash quad (common.h) in the forward and dQ
+// kernels.
 // ============================================================================================
 using mmseq_gemm_detail::rsrc_t;
 using mmseq_gemm_detail::make_rsrc;
@@ -753,13 +754,13 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
 #pragma unroll
   for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
-  const int Tp2 = (T + 1) & ~1;
+  const int Tp4 = (T + 3) & ~3;
   uint64_t drow[2];
-  uint32_t prow[2];  // narrow pair index of (row, key 4g) in tile 0
+  uint32_t prow[2];  // narrow quad index of (row, key 4g) in tile 0
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
-    drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp2;
-    prow[grp] = opaque_u32((uint32_t)(drow[grp] >> 1) + 2 * g);
+    drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp4;
+    prow[grp] = opaque_u32((uint32_t)(drow[grp] >> 2) + g);
   }
   const uint32_t thr1x2 = (a.drop.thr - 1) * 0x10001u, ones2 = opaque_u32(0x10001u);
 
@@ -873,22 +874,24 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
       if (DROP) {  // dropped scores are zeroed in the packed P (one AND per pair of keys), the
                    // 1/(1-p) of the kept ones is applied with the final normalisation.
                    // dword j = 2 kb + q2 of the packed P holds keys 16 kb + 4g + 2 q2 + {0, 1}: the
-                   // two halves of one hash word, keep bits 2j and 2j + 1 of the row's 16-bit slice
+                   // two halves of hash word q2 of the keys' quad (h, then h2), keep bits 2j and
+                   // 2j + 1 of the row's 16-bit slice
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         u32x4 w[2] = {__builtin_bit_cast(u32x4, pf[grp][0]), __builtin_bit_cast(u32x4, pf[grp][1])};
         uint32_t acc = 0;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
           if (kb >= nkb) continue;  // all keys >= T: p = 0, keep bits never read
+          uint32_t hq;
+          if (WIDE) {
+            hq = drop_hash(a.drop, (drow[grp] + t * 64 + kb * 16 + 4 * g) >> 2);
+          } else {  // drop_hash with the quad index < 2^32 (its high word 0)
+            const uint32_t x = ((prow[grp] + (uint32_t)(t * 16 + kb * 4)) ^ a.drop.k0) + a.drop.k1;
+            hq = hash_mixed(x ^ (x >> 16));
+          }
 #pragma unroll
           for (int q2 = 0; q2 < 2; ++q2) {
-            uint32_t hx;
-            if (WIDE) {
-              hx = drop_hash(a.drop, ((drow[grp] + t * 64 + kb * 16 + 4 * g) >> 1) + q2);
-            } else {  // drop_hash with the pair index < 2^32 (its high word 0)
-              const uint32_t x = ((prow[grp] + (uint32_t)(t * 32 + kb * 8 + q2)) ^ a.drop.k0) + a.drop.k1;
-              hx = hash_mixed(x ^ (x >> 16));
-            }
+            const uint32_t hx = q2 ? drop_hash2(hq) : hq;
             const uint32_t k = keep_bits2(hx, thr1x2, ones2);
             const int j = 2 * kb + q2;
             w[kb >> 1][j & 3] &= keep_mask2(k);
@@ -1094,7 +1097,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   }
   const float c = a.scale * LOG2E;
-  const int Tp2 = (T + 1) & ~1;
+  const int Tp4 = (T + 3) & ~3;
   const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + ((int64_t)p * a.heads + h) * T * a.nkt2,
                                               (int64_t)T * a.nkt2 * 8)
                                   : make_rsrc(a.qkv, 0);
@@ -1198,22 +1201,26 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       l[qb] += rs;
       if (DROP) {  // the normaliser keeps the undropped probabilities (dropout after softmax)
         const int q = qw + qb * 32 + r32;
-        // pair index (row base + key) / 2 = dp2 + key / 2: the row base is even and key / 2 < 32,
-        // so the low word never wraps when WIDE is false (checked on the host), and otherwise
-        // the high word takes the carry
-        const uint64_t dp2 = ((((uint64_t)p * a.heads + h) * T + q) * Tp2 + t * 64) >> 1;
-        const uint32_t dlo = (uint32_t)dp2, dhi = (uint32_t)(dp2 >> 32);
+        // quad index (row base + key) / 4 = dp4 + key / 4: the row base is a multiple of 4 and
+        // key / 4 < 16, so the low word never wraps when WIDE is false (checked on the host), and
+        // otherwise the high word takes the carry
+        const uint64_t dp4 = ((((uint64_t)p * a.heads + h) * T + q) * Tp4 + t * 64) >> 2;
+        const uint32_t dlo = (uint32_t)dp4, dhi = (uint32_t)(dp4 >> 32);
         const uint32_t H0 = dhi ^ a.drop.k1, H1 = (dhi + 1u) ^ a.drop.k1;
         const uint32_t thr = a.drop.thr;
         uint32_t wb[2] = {0u, 0u};
+        uint32_t hq = 0;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
           for (int j = 0; j < 16; j += 2) {
-            const int key = kb * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;  // even
-            const uint32_t lo = dlo + (uint32_t)(key >> 1);
-            const uint32_t hw = WIDE ? (lo < dlo ? H1 : H0) : H0;
-            const uint32_t hs = drop_mix((lo ^ a.drop.k0) + hw);  // = drop_hash(pair index)
+            const int key = kb * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;  // even; j & 3: 0 or 2
+            if ((j & 3) == 0) {  // the quad of keys key .. key + 3
+              const uint32_t lo = dlo + (uint32_t)(key >> 2);
+              const uint32_t hw = WIDE ? (lo < dlo ? H1 : H0) : H0;
+              hq = drop_mix((lo ^ a.drop.k0) + hw);  // = drop_hash(quad index)
+            }
+            const uint32_t hs = (j & 3) ? drop_hash2(hq) : hq;
             // all-ones where dropped (half < thr), as plain VALU values: the shift is opaque asm so
             // the compiler cannot turn it into a compare + select (64 lane masks in SGPRs spill)
             const uint32_t d0 = sign_mask((hs & 0xFFFFu) - thr);
@@ -1362,11 +1369,11 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
-  const int Tp2 = (T + 1) & ~1;
+  const int Tp4 = (T + 3) & ~3;
   uint64_t drow[2];
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp)
-    drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp2;
+    drow[grp] = (((uint64_t)p * a.heads + h) * T + (qw + grp * 16 + i)) * Tp4;
   f32x4 dq[2][4];
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp)
@@ -1594,7 +1601,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
-  const int Tp2 = (T + 1) & ~1;
+  const int Tp4 = (T + 3) & ~3;
   f32x4 dk[2][4], dv[2][4], dkt[4], dvt[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
@@ -1622,19 +1629,20 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
                          (wave >> 1) * 2 + ((i >> 3) & 1);
     const uint32_t pos0 = ((i >> 2) & 1) * 16 + (wave & 1) * 8 + (i & 3);
     // DMODE 1: keep bits of this lane's 32 (q, key) elements, bit grp*16 + qs*4 + r, hashed before
-    // the MFMAs (few live registers); (q, key) -> index (rb + q) * Tp2 + key
+    // the MFMAs (few live registers); (q, key) -> index (rb + q) * Tp4 + key
     uint32_t keep = 0xFFFFFFFFu;
     if (DMODE == 1) {
       keep = 0;
-      const uint64_t dbase = (uint64_t)(rb + t * 64 + 4 * g) * (uint64_t)Tp2 + kw + i;
+      const uint64_t dbase = (uint64_t)(rb + t * 64 + 4 * g) * (uint64_t)Tp4 + kw + i;
 #pragma unroll
       for (int grp = 0; grp < 2; ++grp)
 #pragma unroll
         for (int qs = 0; qs < 4; ++qs)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint64_t idx = dbase + (uint64_t)((qs * 16 + r) * Tp2 + grp * 16);
-            const uint32_t h = drop_hash(a.drop, idx >> 1);
+            const uint64_t idx = dbase + (uint64_t)((qs * 16 + r) * Tp4 + grp * 16);
+            const uint32_t hq = drop_hash(a.drop, idx >> 2);
+            const uint32_t h = (idx & 2) ? drop_hash2(hq) : hq;
             const uint32_t u = (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
             keep |= (u >= a.drop.thr ? 1u : 0u) << (grp * 16 + qs * 4 + r);
           }
@@ -1715,14 +1723,14 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
       // DMODE 2: tail key j = i of its tile: bit ((i >> 2) & 1) * 16 + (i & 3), dword (i >> 3) & 1
       const uint32_t* bwt = reinterpret_cast<const uint32_t*>(sBitsT + (t & 1) * 512) + ((i >> 3) & 1);
       const uint32_t post = ((i >> 2) & 1) * 16 + (i & 3);
-      const uint64_t dbt = (uint64_t)(rb + t * 64 + qs * 16 + 4 * g) * (uint64_t)Tp2 + a.tail0 + i;
+      const uint64_t dbt = (uint64_t)(rb + t * 64 + qs * 16 + 4 * g) * (uint64_t)Tp4 + a.tail0 + i;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float pv = ex2(fmaf(st[r], c, kb2t) - Lq[r]);
         float mk = 1.f;
         if (DMODE == 2)
           mk = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)bwt[(qs * 16 + 4 * g + r) * 4], post, 1) & scale_u);
-        if (DMODE == 1) mk = drop_mul(a.drop, dbt + (uint64_t)r * Tp2);
+        if (DMODE == 1) mk = drop_mul(a.drop, dbt + (uint64_t)r * Tp4);
         st[r] = pv * mk;
         dpt[r] = pv * fmaf(dpt[r], mk, -Dq[r]);
       }
@@ -1860,7 +1868,7 @@ static mmseq_status attn_fwd_impl(int P, int T, int Tq, int heads, const void* q
     a.bits = keep_bits;
     a.nkt2 = (nkt + 1) & ~1;
     // largest dropout pair index + the in-tile key offset must stay below 2^32 for the narrow path
-    const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 1) & ~1)) / 2 + 64 >= (1ull << 32);
+    const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 3) & ~3)) / 4 + 64 >= (1ull << 32);
     if (a.drop.thr && keep_bits)
       hipLaunchKernelGGL((wide ? attn_fwd32_kernel<2, true> : attn_fwd32_kernel<2, false>), gq,
                          dim3(128), lds, s, a);
@@ -1879,7 +1887,7 @@ static mmseq_status attn_fwd_impl(int P, int T, int Tq, int heads, const void* q
     a.bits = keep_bits;
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
     // largest dropout pair index + the in-tile key offset must stay below 2^32 for the narrow path
-    const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 1) & ~1)) / 2 + 64 >= (1ull << 32);
+    const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 3) & ~3)) / 4 + 64 >= (1ull << 32);
     if (a.drop.thr && keep_bits)
       hipLaunchKernelGGL((wide ? attn_fwd_bf16_kernel<2, true> : attn_fwd_bf16_kernel<2, false>), gq,
                          dim3(256), lds, s, a);
@@ -2057,7 +2065,7 @@ extern "C" mmseq_status mmseq_attn_fwd_mxfp8_dual(int P, int T, int heads, const
   a.nkt2 = (nkt + 1) & ~1;
   a.bits = keep_bits;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 1) & ~1)) / 2 + 64 >= (1ull << 32);
+  const bool wide = ((uint64_t)P * heads * T * (uint64_t)((T + 3) & ~3)) / 4 + 64 >= (1ull << 32);
   if (a.drop.thr && keep_bits)
     hipLaunchKernelGGL((wide ? attn_fwd_bf16_kernel<2, true, true> : attn_fwd_bf16_kernel<2, false, true>),
                        gq, dim3(256), lds, s, a);

@@ -187,9 +187,13 @@ __device__ __forceinline__ f32x2 gelu_bwd_pair(f32x2 x) {
 }
 
 // --- dropout: counter-based mask (no stored masks; fwd and bwd regenerate the same bits) ---
-// One 32-bit hash per element PAIR (idx >> 1); element idx uses 16-bit half (idx & 1) against a
-// 16-bit threshold round(p * 2^16). The per-call key is derived on the host from (seed, stream)
-// by splitmix64, so streams and seeds are independent; the per-pair mix is Wellons' lowbias32.
+// One 32-bit hash per element QUAD (idx >> 2) decides its four elements: elements 4q and 4q + 1
+// use the low / high 16-bit half of h = lowbias32(key mix of q), elements 4q + 2 and 4q + 3 the
+// halves of h2 = m ^ (m >> 16), m = h * 0x9E3779B1 (one multiply); an element is dropped iff its
+// half < round(p * 2^16). The per-call key is derived on the host from (seed, stream) by
+// splitmix64, so streams and seeds are independent. (Until round 4: one lowbias32 per element
+// PAIR; the quad form halves the hashing with the same 16-bit threshold resolution. Rate, field
+// and lag independence measured in DESIGN §4.2.)
 struct Drop {
   uint32_t thr;     // drop iff half < thr; thr == 0 -> disabled
   uint32_t k0, k1;  // per-call key
@@ -218,10 +222,16 @@ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {  // Wellons' lowbias3
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t pair) {
-  // high word enters by xor + add (no multiply: pair indices here stay below 2^32, and the
+// h of element quad `quad`
+__device__ __forceinline__ uint32_t drop_hash(const Drop& d, uint64_t quad) {
+  // high word enters by xor + add (no multiply: quad indices here stay below 2^32, and the
   // lowbias32 rounds provide the diffusion)
-  return drop_mix(((uint32_t)pair ^ d.k0) + ((uint32_t)(pair >> 32) ^ d.k1));
+  return drop_mix(((uint32_t)quad ^ d.k0) + ((uint32_t)(quad >> 32) ^ d.k1));
+}
+// h2: the quad's second 32 bits (elements 4q + 2, 4q + 3)
+__device__ __forceinline__ uint32_t drop_hash2(uint32_t h) {
+  const uint32_t m = h * 0x9E3779B1u;
+  return m ^ (m >> 16);
 }
 __device__ __forceinline__ float drop_sel(const Drop& d, uint32_t h, int hi) {
   const uint32_t u = hi ? (h >> 16) : (h & 0xFFFFu);
@@ -230,20 +240,33 @@ __device__ __forceinline__ float drop_sel(const Drop& d, uint32_t h, int hi) {
 // multiplier for element idx: 0 (dropped) or 1/(1-p); 1 when disabled
 __device__ __forceinline__ float drop_mul(const Drop& d, uint64_t idx) {
   if (d.thr == 0) return 1.f;
-  return drop_sel(d, drop_hash(d, idx >> 1), (int)(idx & 1));
+  const uint32_t h = drop_hash(d, idx >> 2);
+  return drop_sel(d, (idx & 2) ? drop_hash2(h) : h, (int)(idx & 1));
 }
-// multipliers for elements idx .. idx + 2n - 1 with idx EVEN (one hash per pair)
+// multipliers for elements idx .. idx + 2n - 1 with idx EVEN (one hash per quad when idx % 4 == 0)
 template <int NPAIR>
 __device__ __forceinline__ void drop_mul_pairs(const Drop& d, uint64_t idx, float* m) {
-  const uint64_t j = idx >> 1;
+  if ((NPAIR % 2) == 0 && (idx & 3) == 0) {
 #pragma unroll
-  for (int q = 0; q < NPAIR; ++q) {
-    const uint32_t h = drop_hash(d, j + q);
-    m[2 * q] = drop_sel(d, h, 0);
-    m[2 * q + 1] = drop_sel(d, h, 1);
+    for (int q = 0; q < NPAIR / 2; ++q) {
+      const uint32_t h = drop_hash(d, (idx >> 2) + q), h2 = drop_hash2(h);
+      m[4 * q] = drop_sel(d, h, 0);
+      m[4 * q + 1] = drop_sel(d, h, 1);
+      m[4 * q + 2] = drop_sel(d, h2, 0);
+      m[4 * q + 3] = drop_sel(d, h2, 1);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NPAIR; ++q) {
+      const uint64_t j = (idx >> 1) + q;  // element pair j = elements 2j, 2j + 1
+      const uint32_t h = drop_hash(d, j >> 1);
+      const uint32_t w = (j & 1) ? drop_hash2(h) : h;
+      m[2 * q] = drop_sel(d, w, 0);
+      m[2 * q + 1] = drop_sel(d, w, 1);
+    }
   }
 }
-// multipliers for the 4 elements idx .. idx + 3 (pair-shared hashes when idx is even)
+// multipliers for the 4 elements idx .. idx + 3 (one hash when idx % 4 == 0)
 __device__ __forceinline__ void drop_mul4(const Drop& d, uint64_t idx, float* m) {
   if (d.thr == 0) {
     m[0] = m[1] = m[2] = m[3] = 1.f;

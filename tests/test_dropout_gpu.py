@@ -127,8 +127,8 @@ def test_attention_dropout_fwd_bwd(dtype, P, T, heads, masked, bits, fast):
     nat.attn_set_fast(fast)
     nat.attn_fwd(P, T, heads, qkv, 3 * H, 0, H, 2 * H, bias, scale, out, H, lse, drop=d, keep_bits=kb)
     nat.attn_set_fast(1)
-    Tp2 = (T + 1) & ~1  # attention mask rows are laid out with an even stride
-    Mk = _mask((P, heads, T, Tp2), d)[..., :T]
+    Tp4 = (T + 3) & ~3  # attention mask rows: stride T rounded up to a multiple of 4 (hash quads)
+    Mk = _mask((P, heads, T, Tp4), d)[..., :T]
     qf = qkv.float().requires_grad_(True)
     q, k, v = qf.view(P, T, 3, heads, 64).unbind(2)
     s = torch.einsum("pqhd,pkhd->phqk", q, k) * scale

@@ -1,0 +1,91 @@
+"""Pick the config-5 MX-fp8 decisive-ordering fixture's weight scaling (tests/golden/
+make_golden_real.py DECISIVE_SCALE["decisive_config5_l2"]): at the real_config5_l2 shape (ViT-L/14 +
+1024-wide joint encoder, 2 + 2 layers, N = 9, T = 769), for candidate scalings of the pointer head,
+the fp32 model's beam order O*, its NLL margin over the 36 orders one transposition away, and the
+MX-fp8 eval forward's (kernels.fp8_forward) error on those margins. N = 9 has 9! orders, so the
+margin is taken over that neighbourhood. Measurement only."""
+import itertools
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")]
+from counter_init import counter_state_dict  # noqa: E402
+from make_golden_real import CONFIG5_L2, real_inputs  # noqa: E402
+from multimodal_sequencing_amd import kernels as K  # noqa: E402
+from multimodal_sequencing_amd import model_zoo  # noqa: E402
+from multimodal_sequencing_amd.berson import berson_pointer_network  # noqa: E402
+
+CANDIDATES = {
+    "tl50_q50_kl50": {"tanh_linear.weight": 50, "query_linear.weight": 50, "key_linear.weight": 50},
+    "tl100_q100_kl100": {"tanh_linear.weight": 100, "query_linear.weight": 100, "key_linear.weight": 100},
+    "tl200_q50_kl50": {"tanh_linear.weight": 200, "query_linear.weight": 50, "key_linear.weight": 50},
+    "tl50_q200_kl200": {"tanh_linear.weight": 50, "query_linear.weight": 200, "key_linear.weight": 200},
+}
+
+
+def model(cfg, dtype, scale, bf16w=False):
+    m = model_zoo.build_from_golden(cfg, device="cuda", dtype=dtype)
+    sd = counter_state_dict({k: tuple(v.shape) for k, v in m.state_dict().items()})
+    for k, f in scale.items():
+        sd[k] = sd[k] * f
+    if bf16w:
+        sd = {k: (torch.from_numpy(v).bfloat16().float().numpy() if v.dtype == np.float32 else v)
+              for k, v in sd.items()}
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.eval()
+    return m
+
+
+def nll(m, inp, order):
+    with torch.no_grad():
+        m({**inp, "labels": torch.tensor([list(order)])})
+    return float(m.last_loss_terms[0]) * (len(order) - 1)
+
+
+def neighbours(order):
+    out = []
+    for a, b in itertools.combinations(range(len(order)), 2):
+        o = list(order)
+        o[a], o[b] = o[b], o[a]
+        out.append(o)
+    return out
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    names = sys.argv[2:] or list(CANDIDATES)
+    cfg = dict(CONFIG5_L2, B=B)
+    ids, labels, images = real_inputs(320, cfg)
+    for sname in names:
+        scale = CANDIDATES[sname]
+        m32, m16 = model(cfg, torch.float32, scale), model(cfg, torch.bfloat16, scale)
+        dec = 0
+        for b in range(B):
+            inp = {"input_ids": torch.from_numpy(ids[b:b + 1]),
+                   "labels": torch.from_numpy(labels[b:b + 1]),
+                   "images": torch.from_numpy(images[b:b + 1]).cuda()}
+            with torch.no_grad():
+                best = berson_pointer_network(m32.args, m32, None, inp)
+                with K.fp8_forward():
+                    o8 = berson_pointer_network(m16.args, m16, None, inp)
+            nb = neighbours(best)
+            n32 = [nll(m32, inp, o) for o in [best] + nb]
+            with K.fp8_forward():
+                n8 = [nll(m16, inp, o) for o in [best] + nb]
+            gap32 = np.array(n32[1:]) - n32[0]
+            gap8 = np.array(n8[1:]) - n8[0]
+            margin = float(gap32.min())
+            err = float(np.abs(gap8 - gap32).max())
+            ok = margin > 5 * err
+            dec += ok
+            print(f"{sname} story {b}: margin {margin:.3f} fp8 err {err:.3f} (x{margin / max(err, 1e-9):.1f}) "
+                  f"fp32 order {best} fp8 order {o8} {'DECISIVE' if ok else ''}", flush=True)
+        print(f"{sname}: {dec}/{B} decisive", flush=True)
+
+
+if __name__ == "__main__":
+    main()
