@@ -165,6 +165,39 @@ __device__ __forceinline__ float gelu_sig(float x) {
   const float q = xc * fmaf(x2, fmaf(x2, K2, K1), K0);  // -log2(e) * x (c0 + c1 x^2 + c2 x^4)
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(q));
 }
+// gelu_sig on 8 values as packed fp32 pairs (v_pk_mul / v_pk_fma / v_pk_add_f32: the same fp32
+// operations in the same order, so bit-identical to gelu_sig per element): for the GEMM epilogues,
+// where no MFMA runs beside them (beside MFMAs packed fp32 costs more than two scalar ops,
+// MI355X_MICROARCH.md, which is why the rest of the library builds with -fno-slp-vectorize)
+__device__ __forceinline__ void gelu_sig8(float* v) {
+  constexpr float L2E = 1.4426950408889634f;
+  constexpr float K0 = -1.59501577f * L2E, K1 = -7.40112921e-2f * L2E, K2 = 7.03033584e-4f * L2E;
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    const f32x2 x = {v[r], v[r + 1]};
+    const f32x2 xc = {__builtin_amdgcn_fmed3f(x[0], -9.f, 9.f), __builtin_amdgcn_fmed3f(x[1], -9.f, 9.f)};
+    const f32x2 x2 = xc * xc;
+    const f32x2 t = __builtin_elementwise_fma(x2, __builtin_elementwise_fma(x2, (f32x2){K2, K2}, (f32x2){K1, K1}),
+                                              (f32x2){K0, K0});
+    const f32x2 q = xc * t;
+    const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])} + (f32x2){1.0f, 1.0f};
+    const f32x2 y = x * (f32x2){__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    v[r] = y[0];
+    v[r + 1] = y[1];
+  }
+}
+// bias + alpha for 8 accumulators as packed pairs: v = acc * alpha + bias (fmaf per element)
+__device__ __forceinline__ void bias_alpha8(float* v, const f32x4& lo, const f32x4& hi, float alpha,
+                                            const f32x4& b0, const f32x4& b1) {
+  const f32x2 al = {alpha, alpha};
+#pragma unroll
+  for (int r = 0; r < 4; r += 2) {
+    const f32x2 a = __builtin_elementwise_fma((f32x2){lo[r], lo[r + 1]}, al, (f32x2){b0[r], b0[r + 1]});
+    const f32x2 c = __builtin_elementwise_fma((f32x2){hi[r], hi[r + 1]}, al, (f32x2){b1[r], b1[r + 1]});
+    v[r] = a[0]; v[r + 1] = a[1];
+    v[4 + r] = c[0]; v[4 + r + 1] = c[1];
+  }
+}
 // derivative of gelu_sig's function (the backward of the forward actually computed): s + x s (1 - s)
 // p'(x), p' = c0 + 3 c1 x^2 + 5 c2 x^4; max abs error vs the exact GELU' 1.1e-4
 __device__ __forceinline__ float gelu_sig_grad(float x) {

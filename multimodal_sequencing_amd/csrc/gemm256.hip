@@ -94,10 +94,14 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
                                      const EpiBias& bias, const float MMSEQ_LDS* dtab = nullptr) {
   if (CHK && (m >= a.M || n >= a.N)) return;
   float v[8];
+  if (XIN) {  // scalar: the operand-reading variants sit at 256 VGPRs (packed pairs spill there)
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
-    v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
+    for (int r = 0; r < 4; ++r) {
+      v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
+      v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
+    }
+  } else {
+    bias_alpha8(v, lo, hi, a.alpha, bias.b0, bias.b1);
   }
 #ifdef MMSEQ_EPI_SINK  // experiment: every tile stores into rows 0-255 (L2-resident, no HBM writes)
   const int64_t off = (int64_t)(m & 255) * a.ldc + n;
@@ -118,14 +122,15 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int m, int n, f32x4 lo, 
   } else if (ACT) {
     if (a.aux) st8(reinterpret_cast<us*>(a.aux) + off, v);
     if (ACT == MMSEQ_ACT_GELU_ERF) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
+      gelu_sig8(v);
     } else {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
     }
   }
-  if (a.drop.thr) {  // m * N + n is even (N % 8 == 0, n % 8 == 0): one hash per pair
+  if (!BWD && a.drop.thr) {  // m * N + n % 8 == 0 (N % 8 == 0, n % 8 == 0): one hash per quad;
+    // the dgrad variants take no dropout (the host sends those to the generic kernels), which
+    // keeps them off scratch (4 spilled VGPRs with the hash compiled in)
     float dm[8];
     drop_mul_pairs<4>(a.drop, (uint64_t)m * a.N + n, dm);
 #pragma unroll
@@ -150,11 +155,7 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
                                         const EpiBias& bias, const EpiIn* din = nullptr,
                                         const float MMSEQ_LDS* dtab = nullptr) {
   float v[8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = fmaf(lo[r], a.alpha, bias.b0[r]);
-    v[4 + r] = fmaf(hi[r], a.alpha, bias.b1[r]);
-  }
+  bias_alpha8(v, lo, hi, a.alpha, bias.b0, bias.b1);
   const bool in = m < a.M && n < a.N;
   const int64_t offb = (int64_t)m * a.ldcb + n;
   if (BWD) {
@@ -163,8 +164,7 @@ __device__ __forceinline__ void epi8_q8(const GemmArgs& a, int m, int n, int g, 
   } else {
     if (ACT && a.aux && in) st8(reinterpret_cast<us*>(a.aux) + offb, v);  // training: pre-activation
     if (ACT == MMSEQ_ACT_GELU_ERF) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
+      gelu_sig8(v);
     } else if (ACT) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
@@ -1261,11 +1261,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a, int tiles_n
           const f32x4 b0 = *reinterpret_cast<const f32x4*>(sbr + cn);
           const f32x4 b1 = *reinterpret_cast<const f32x4*>(sbr + cn + 4);
           float v[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = fmaf(lo[r], a.alpha, b0[r]);
-            v[4 + r] = fmaf(hi[r], a.alpha, b1[r]);
-          }
+          bias_alpha8(v, lo, hi, a.alpha, b0, b1);
           u16x8 xin = (u16x8){0, 0, 0, 0, 0, 0, 0, 0};
           if (NL) xin = __builtin_bit_cast(u16x8, in[c & 1][q]);
           if (BWD) {
@@ -1279,14 +1275,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a, int tiles_n
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, z), rX, call_off(call, a.ldc), 0, 0);
             }
             if (ACT == MMSEQ_ACT_GELU_ERF) {
-#pragma unroll
-              for (int r = 0; r < 8; ++r) v[r] = gelu_sig(v[r]);
+              gelu_sig8(v);
             } else {
 #pragma unroll
               for (int r = 0; r < 8; ++r) v[r] = act_fwd_fast(ACT, v[r]);
             }
           }
-          if (a.drop.thr) {
+          if (!BWD && a.drop.thr) {
             const int m = m0 + wr * 128 + i * 16 + ii;
             float dm[8];
             drop_mul_pairs<4>(a.drop, (uint64_t)m * a.N + (n0 + cn), dm);
@@ -1336,7 +1331,7 @@ bool mmseq_gemm256_nt(const GemmArgs& a, bool out_bf16, int num_cu, hipStream_t 
                       int variant, int delay) {
   auto a16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!out_bf16 || a.K % 128 != 0 || a.splitk != 1 || a.N % 8 != 0 || a.ldc % 8 != 0 ||
-      (a.accumulate && (a.resid || a.dact)) ||
+      (a.accumulate && (a.resid || a.dact)) || (a.dact && a.drop.thr) ||
       (a.resid && (a.ldr % 8 != 0 || !a16(a.resid))) || !a16(a.C) || (a.aux && !a16(a.aux)) ||
       (a.dact && !a16(a.dact)))
     return false;
