@@ -17,7 +17,8 @@ the product's full-depth drift equals that of an ideal bf16 placement of the sam
 dominant term is the bf16 rounding of the WEIGHT operands — a systematic perturbation of the
 model that the span pooling does not average out (pointer keys 3.5e-3 relative from it alone; all
 the activation roundings together give 1e-3). `decisive_config3_bf16w` holds 8 stories whose
-weights are bf16-representable, so there the margin error measures the activation arithmetic alone.
+weights are bf16-representable, so there the margin error measures the activation arithmetic alone
+(16 stories; three quarters of them must be decisive).
 """
 import json
 import os
@@ -109,4 +110,9 @@ def test_decisive_order_bf16_exact(name):
         if margin > DECISIVE * err:
             decisive += 1
             assert order == ref, (name, b, order, ref, margin, err)
-    assert decisive >= (n + 1) // 2, (name, decisive, n)  # the check is not vacuous
+    # the check is not vacuous: at least half of every fixture's stories are decisive, and three
+    # quarters of the 16 bf16-weight stories (their margin errors measure the activation
+    # arithmetic alone)
+    need = (3 * n + 3) // 4 if name == "decisive_config3_bf16w" else (n + 1) // 2
+    print(f"{name}: {decisive} of {n} stories decisive (need {need})")
+    assert decisive >= need, (name, decisive, n)

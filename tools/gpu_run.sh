@@ -9,6 +9,7 @@
 #   smoke            __graft_entry__.smoke()                          -> smoke.log
 #   bench[:ARGS]     python bench.py ARGS                             -> bench.log (appended)
 #   py:SCRIPT ARGS   python SCRIPT ARGS                               -> <script>.log (appended)
+#   bin:PROG ARGS    a program built here beforehand (e.g. tools/bw_mix) -> <prog>.log (appended)
 #   attn-ab:NAME     rocprof kernel stats of tools/attn_bench.py, ab/libmmseq_NAME.so vs the
 #                    tree, alternated twice                           -> attn_{NAME,tree}_stats.csv
 #   epi-ab:NAME      tools/gemm_epi_bench.py, NAME vs tree, twice     -> epi_{NAME,tree}.log
@@ -56,6 +57,9 @@ for step in "$@"; do
     py)
       s=$(basename "${arg%% *}" .py)
       timeout -k 10 600 python -u $arg >> "$out/$s.log" 2>&1 ;;
+    bin)
+      s=$(basename "${arg%% *}")
+      timeout -k 10 300 $arg >> "$out/$s.log" 2>&1 ;;
     attn-ab|epi-ab|bench-ab)
       for v in "$arg" tree "$arg" tree; do
         with_lib "$v"
