@@ -680,6 +680,256 @@ __device__ __forceinline__ uint32_t hash_mixed(uint32_t x) {  // drop_mix with t
   return x ^ (x >> 16);
 }
 
+// Forward tail block: the last query block of a (pair, head) when it holds 1-16 rows (T % 128 in
+// [1, 16]: T = 513 leaves 1, the ViT's T = 393 leaves 9). Those rows are one 16-row MFMA group, and
+// one wave sweeping all T keys for them kept the whole workgroup slot for as long as a full block
+// while three of its waves idled. Here the four waves split the keys instead: 32-key chunk c goes
+// to wave c % 4, which stages it by LDS-DMA into its own 8 KB of the K / V ring (K rows at +0, V at
+// +4 KB: the first 32 rows of the 64-key image layout, so the fragment offsets are the main loop's)
+// and runs the same online softmax / dropout / P V on it. The four partial (m, l, O) then merge in
+// wave order through LDS (exact for any reference m: O and l are relative to their own m).
+// Per score the arithmetic is the main loop's (same scale, bias, hash index, keep decision); only
+// the order of the key-chunk sums differs.
+template <int DMODE, bool WIDE, bool Q8>
+__device__ __forceinline__ void attn_fwd_tail(const AttnArgs& a, unsigned short* smem, int p, int h,
+                                              int q0) {
+  constexpr bool DROP = DMODE != 0;
+  float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int T = a.T;
+  const int nkt = (T + 63) >> 6, nch = (T + 31) >> 5;
+  const int64_t ld = a.ld_qkv;
+  const rsrc_t rk = head_rsrc(a.qkv, (int64_t)p * T, ld, a.k_off + h * 64, T);
+  const rsrc_t rv = head_rsrc(a.qkv, (int64_t)p * T, ld, a.v_off + h * 64, T);
+  const uint32_t loff = dma_lane_off(lane, ld);
+  unsigned short* kimg = smem + wave * 4096;  // this wave's 8 KB: K rows 0-31, then V rows 0-31
+  unsigned short* vimg = kimg + 2048;
+  auto stage = [&](int c) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t vo = loff + (uint32_t)((int64_t)(c * 32 + e * 8) * ld * 2);
+      dma16(rk, kimg + e * 512, vo);
+      dma16(rv, vimg + e * 512, vo);
+    }
+  };
+  if (wave < nch) stage(wave);
+  const float* kbias = a.key_bias ? a.key_bias + (int64_t)p * T : nullptr;
+  int* sZero = reinterpret_cast<int*>(sBias + nkt * 64);
+  const rsrc_t rkb = make_rsrc(kbias, kbias ? (int64_t)T * 4 : 0);
+  for (int tt = wave; tt < nkt; tt += 4) {
+    const int k = tt * 64 + lane;
+    const float bv = k < T ? buf_f32(rkb, k) * LOG2E : -1e30f;
+    sBias[k] = bv;
+    const bool z = __ballot(bv != 0.f) == 0;
+    if (lane == 0) sZero[tt] = z;
+  }
+  const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
+  bf16x8_t qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qf[ks] = buf_row_frag(rq, q0 + i, ld, ks, lane);
+  const rsrc_t rbits = DMODE == 2 ? make_rsrc(a.bits + ((int64_t)p * a.heads + h) * T * a.nkt2,
+                                              (int64_t)T * a.nkt2 * 8)
+                                  : make_rsrc(a.qkv, 0);
+  const uint32_t boff0 = (uint32_t)(((q0 + i) * a.nkt2 * 4 + g) * 2);
+  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
+  const float c = a.scale * LOG2E;
+  const uint64_t drow = (((uint64_t)p * a.heads + h) * T + (q0 + i)) * (uint64_t)((T + 3) & ~3);
+  const uint32_t prow = opaque_u32((uint32_t)(drow >> 2) + g);
+  const uint32_t thr1x2 = (a.drop.thr - 1) * 0x10001u, ones2 = opaque_u32(0x10001u);
+  const bf16x8_t ones = bf16_ones();
+  f32x4 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f;
+  f32x4 lsum = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // key bias of every tile in LDS
+  for (int ch = wave; ch < nch; ch += 4) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's chunk landed (its own DMA)
+    const int t = ch >> 1, half = ch & 1;
+    const int nkb = min(2, (T - ch * 32 + 15) >> 4);  // 16-key blocks holding a valid key
+    f32x4 s[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk < nkb) {
+        const bf16x8_t k0 = lds_row(kimg, kk * 1024 + ro0), k1 = lds_row(kimg, kk * 1024 + ro1);
+        s[kk] = mma(k1, qf[1], mma(k0, qf[0], (f32x4){0.f, 0.f, 0.f, 0.f}));
+      } else {
+        s[kk] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    const bool zb = __builtin_amdgcn_readfirstlane(sZero[t]) != 0;
+    float mx = -1e30f;
+    if (zb) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kk][r]);
+      mx *= c;
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk >= nkb) continue;
+        const f32x4 b = *reinterpret_cast<const f32x4*>(sBias + t * 64 + (2 * half + kk) * 16 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = fmaf(s[kk][r], c, b[r]);
+          s[kk][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      }
+    }
+    if (__ballot(mx > m + 8.f) != 0) {
+      const float mn = fmaxf(m, xlane_max4(mx));
+      const float alpha = ex2(m - mn);
+      m = mn;
+      lsum *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    }
+    if (zb) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kk][r] = ex2(fmaf(s[kk][r], c, -m));
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk >= nkb) {
+          s[kk] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kk][r] = ex2(s[kk][r] - m);
+      }
+    }
+    bf16x8_t pf = pack_pair(s[0], s[1]);
+    lsum = mma(ones, pf, lsum);
+    if (DROP) {  // as the main loop: dword j = 2 kk + q2 of pf is kb = 2 half + kk of tile t
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 w = __builtin_bit_cast(u32x4, pf);
+      uint32_t acc = 0;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk >= nkb) continue;
+        const int kb = 2 * half + kk;
+        uint32_t hq;
+        if (WIDE) {
+          hq = drop_hash(a.drop, (drow + t * 64 + kb * 16 + 4 * g) >> 2);
+        } else {
+          const uint32_t x = ((prow + (uint32_t)(t * 16 + kb * 4)) ^ a.drop.k0) + a.drop.k1;
+          hq = hash_mixed(x ^ (x >> 16));
+        }
+#pragma unroll
+        for (int q2 = 0; q2 < 2; ++q2) {
+          const uint32_t hx = q2 ? drop_hash2(hq) : hq;
+          const uint32_t k = keep_bits2(hx, thr1x2, ones2);
+          w[2 * kk + q2] &= keep_mask2(k);
+          if (DMODE == 2) acc |= k << (2 * (2 * kb + q2));
+        }
+      }
+      pf = __builtin_bit_cast(bf16x8_t, w);
+      if (DMODE == 2) {  // byte `half` of the row's 16-bit slice g of tile t (the other byte is
+                         // the other chunk's, written by another wave)
+        const uint32_t kb16 = (acc & 0x5555u) | ((acc >> 15) & 0xAAAAu);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(kb16 >> (8 * half)), rbits,
+                                             boff0 + t * 8 + half, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = mma(lds_tr(vimg, to[d]), pf, o[d]);
+    if (ch + 4 < nch) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this chunk's LDS reads done
+      stage(ch + 4);
+    }
+  }
+  // merge: wave w's (m, l, O) for its lane at float [w][lane][0..17] of the K / V ring
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's LDS reads (and DMA) done before the ring is overwritten
+  float* sM = reinterpret_cast<float*>(smem);
+  float* mine = sM + (wave * 64 + lane) * 18;
+  mine[0] = m;
+  mine[1] = lsum[0];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mine[2 + 4 * d + r] = o[d][r];
+  __syncthreads();
+  if (wave != 0) return;
+  float mw[4], M = -1e30f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    mw[w] = sM[(w * 64 + lane) * 18];
+    M = fmaxf(M, mw[w]);
+  }
+  float L = 0.f;
+  f32x4 O[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) O[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float* src = sM + (w * 64 + lane) * 18;
+    const float sc = ex2(mw[w] - M);
+    L = fmaf(src[1], sc, L);
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) O[d][r] = fmaf(src[2 + 4 * d + r], sc, O[d][r]);
+  }
+  const int q = q0 + i;
+  if (q < a.Tq) {
+    const float inv = (DROP ? a.drop.scale : 1.0f) / L;
+    if (Q8) {  // as the main loop's MX-fp8 output (and the training forward's bf16 copy)
+      const int64_t row = (int64_t)p * a.Tq + q;
+      const int KB = a.heads * 2;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float v[8], amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = bf2f(f2bf(O[2 * b + (e >> 2)][e & 3] * inv));
+          amax = fmaxf(amax, fabsf(v[e]));
+        }
+        amax = xlane_max4(amax);
+        int ex = amax > 0.f ? (int)((__float_as_uint(amax) >> 23) & 0xff) - 127 : -127;
+        ex = max(-127, min(127, ex - 8));
+        const float sc = ldexpf(1.f, -ex);
+        if (g == 0)
+          a.q8s[((row >> 6) * KB + h * 2 + b) * 64 + (row & 15) * 4 + ((row >> 4) & 3)] = (uint8_t)(ex + 127);
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+          const float s0 = fminf(448.f, fmaxf(-448.f, v[4 * dd] * sc));
+          const float s1 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 1] * sc));
+          const float s2 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 2] * sc));
+          const float s3 = fminf(448.f, fmaxf(-448.f, v[4 * dd + 3] * sc));
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+          pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+          *reinterpret_cast<int*>(a.q8 + row * a.ldq8 + h * 64 + (2 * b + dd) * 16 + 4 * g) = pk;
+        }
+        if (a.o_w) {
+          unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + row * a.ld_out + h * 64 + 4 * g;
+#pragma unroll
+          for (int dd = 0; dd < 2; ++dd) {
+            typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+            *reinterpret_cast<u16x4*>(op + (2 * b + dd) * 16) =
+                (u16x4){f2bf(v[4 * dd]), f2bf(v[4 * dd + 1]), f2bf(v[4 * dd + 2]), f2bf(v[4 * dd + 3])};
+          }
+        }
+      }
+    } else {
+      unsigned short* op = reinterpret_cast<unsigned short*>(a.o_w) + ((int64_t)p * a.Tq + q) * a.ld_out +
+                           h * 64 + 4 * g;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) Vec4<unsigned short>::st(op + d * 16, O[d] * inv);
+    }
+    if (g == 0) a.lse[((int64_t)p * a.heads + h) * T + q] = (M + __builtin_amdgcn_logf(L)) * LN2;
+  }
+}
+
 template <int DMODE, bool WIDE, bool Q8 = false>  // dropout: 0 none, 1 counter hash, 2 counter
                                  // hash + keep bits out; WIDE: dropout pair indices >= 2^32 (64-bit
                                  // index arithmetic); Q8: MX-fp8 output (eval, the O-proj operand)
@@ -696,6 +946,13 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
   const int T = a.T;
   const BlkIdx bi = attn_block((a.Tq + 127) >> 7, a.heads);
   const int h = bi.h, p = bi.p;
+#ifndef MMSEQ_ATTN_NO_TAIL
+  // the last 1-16 rows of T (bit-identical whether or not the launch covers only Tq < T rows)
+  if (((T - 1) & 127) < 16 && bi.x == (T - 1) >> 7) {
+    attn_fwd_tail<DMODE, WIDE, Q8>(a, smem, p, h, bi.x * 128);
+    return;
+  }
+#endif
   const int nkt = (T + 63) >> 6;
   const int qw = bi.x * 128 + wave * 32;
   const bool active = qw < a.Tq;

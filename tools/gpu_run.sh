@@ -21,6 +21,8 @@
 #   lib-ab:NAME:SCRIPT ARGS  python SCRIPT ARGS with ab/libmmseq_NAME.so vs the tree, alternated
 #                    twice (e.g. lib-ab:base:tools/ln_bench.py bwd)   -> <script>_{NAME,tree}.log
 #   profile          tools/profile_round.sh TAG (kernel stats + PMC of the default bench)
+#   dp2-gloo         the 2-rank data-parallel path on this one GPU over gloo (4 stories per rank,
+#                    the bench line with its all-reduce diagnostics) -> bench_dp2_gloo.log
 set -euo pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 tag=${1:?tag}; shift
@@ -95,6 +97,10 @@ for step in "$@"; do
       unset MMSEQ_BENCH_LIB ;;
     profile)
       bash tools/profile_round.sh "$tag" ;;
+    dp2-gloo)
+      timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --dist-backend gloo \
+        --batch 4 --micro 4 --steps 3 --warmup 1 $short --fwd-steps 0 > "$out/bench_dp2_gloo.log" 2>&1 ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done
