@@ -343,8 +343,14 @@ def bench_config5(stories, micro, steps, warmup, dev):
     torch.cuda.empty_cache()
     out = {"workload": f"config5 shape: ViT-L/14 + 24x1024 joint encoder + BERSON, N={Nst}, "
                        f"{Nst * (Nst - 1)} pairs/story, pair seq {2 * per}+{Tv}={2 * per + Tv}, "
-                       f"{stories} stories/step in micro-batches of {micro}, train mode (dropout), 1 GPU",
+                       f"{stories} stories/step in micro-batches of {micro}, train mode (dropout), 1 GPU; "
+                       f"the last joint layer runs on the text rows only"
+                       f"{' (in bf16 under fp8_forward)' if K.ROWS['on'] else ' (off: MMSEQ_ROWS=0)'}",
            **train["bf16"], "fwd_tflop_per_story": fwd / 1e12,
+           "loss_note": "the three training legs run one after another on one model and optimizer "
+                        "(bf16, then mxfp8_fwd, then mxfp8_fwd_dgrad), so each leg's loss is after "
+                        "a different number of updates and the training losses are not comparable "
+                        "across legs; eval_forward's two losses are (same weights, same batch)",
            "train_mxfp8_forward": dict(train["mxfp8_fwd"], speedup=train["mxfp8_fwd"]["steps_per_s"] /
                                        train["bf16"]["steps_per_s"],
                                        mode="kernels.fp8_forward(training=True): the four encoder "
