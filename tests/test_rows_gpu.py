@@ -35,7 +35,9 @@ def _qkv(P, T, heads, seed):
 
 @pytest.mark.parametrize("P,T,Tq,heads,mode", [(3, 513, 120, 2, "bits"), (2, 393, 200, 4, "none"),
                                                (2, 769, 257, 2, "hash"), (1, 300, 1, 2, "bits"),
-                                               (2, 160, 160, 2, "bits")])
+                                               (2, 160, 160, 2, "bits"),
+                                               # Tq inside the forward's tail block of T (rows 256-271)
+                                               (2, 272, 270, 2, "bits"), (1, 513, 513, 2, "none")])
 def test_attention_rows_equal_full(P, T, Tq, heads, mode):
     """mmseq_attn_fwd_rows / _bwd_rows against mmseq_attn_fwd / _bwd (variant 1) with the dO rows
     past Tq zero: O, LSE and keep bits of rows < Tq, and the whole dQ|dK|dV (dQ = 0 past Tq),
