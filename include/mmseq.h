@@ -259,6 +259,22 @@ mmseq_status mmseq_layernorm_bwd_rows(int rows, int cols, const void* dy, mmseq_
                                       mmseq_dtype dtype, const mmseq_dropout* drop_dy,
                                       void* dx_drop, mmseq_rows dx_dropl,
                                       const mmseq_dropout* drop_dx, mmseq_stream stream);
+/* layernorm_bwd_ex: mmseq_layernorm_bwd_rows (dx_drop optional, in its own layout dx_dropl) that
+ *  also ACCUMULATES into dsum[cols] the column sums of the gradient it writes for the next GEMM —
+ *  dx_drop when given, else dx (with dres) — as stored (bf16-rounded in bf16): the bias gradient of
+ *  the Linear whose output gradient that is (BertSelfOutput / BertOutput dense and the CLIP
+ *  attention out_proj, lxrt/modeling.py:431-433,489-493, clip/model.py:219-221), so that its
+ *  weight-gradient GEMM runs without the fused bias pass (mmseq_gemm_wgrad with gb = NULL). The
+ *  summed gradient must be in dense rows. Summed in a fixed order (bitwise repeatable). Same
+ *  workspace as mmseq_layernorm_bwd. dsum = NULL: exactly mmseq_layernorm_bwd(_rows). */
+mmseq_status mmseq_layernorm_bwd_ex(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                    const void* x, mmseq_rows xl, const float* mean,
+                                    const float* rstd, const float* gamma, void* dx,
+                                    mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                    float* dgamma, float* dbeta, float* workspace,
+                                    mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                    void* dx_drop, mmseq_rows dx_dropl,
+                                    const mmseq_dropout* drop_dx, float* dsum, mmseq_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused text embedding + LayerNorm written straight into the joint buffer (BertEmbeddings,

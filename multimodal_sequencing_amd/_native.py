@@ -109,6 +109,9 @@ _SIGS = {
     "mmseq_layernorm_bwd_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
                                                 _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
                                                 ctypes.c_int, _dp, _vp, Rows, _dp, _vp]),
+    "mmseq_layernorm_bwd_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows, _vp,
+                                              _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
+                                              ctypes.c_int, _dp, _vp, Rows, _dp, _vp, _vp]),
     "mmseq_layernorm_bwd_mxfp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, Rows, _vp, Rows,
                                                  _vp, _vp, _vp, _vp, Rows, _vp, Rows, _vp, _vp, _vp,
                                                  _dp, _vp, _dp, _vp, _c_i64, _vp, _vp]),
@@ -377,10 +380,20 @@ def layernorm_fwd_mxfp8(nrows, cols, x, gamma, beta, eps, y=None, mean=None, rst
 
 
 def layernorm_bwd(nrows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl, dgamma,
-                  dbeta, drop_dy=None, dx_drop=None, drop_dx=None, dx_drop_rows=None):
-    """dx_drop_rows: the row layout of dx_drop (mmseq_layernorm_bwd_rows); default dx's."""
+                  dbeta, drop_dy=None, dx_drop=None, drop_dx=None, dx_drop_rows=None, dsum=None):
+    """dx_drop_rows: the row layout of dx_drop (mmseq_layernorm_bwd_rows); default dx's. dsum:
+    fp32 [cols] += column sums of the gradient written for the next GEMM (dx_drop, else dx) — the
+    next Linear's bias gradient (mmseq_layernorm_bwd_ex)."""
     ws = torch.empty(lib().mmseq_layernorm_bwd_workspace(nrows, cols), dtype=torch.float32,
                      device=x.device)
+    if dsum is not None:
+        _dev(dsum)
+        _check(lib().mmseq_layernorm_bwd_ex(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
+                                            _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),
+                                            _p(dbeta), _p(ws), dt(x), _d(drop_dy), _p(dx_drop),
+                                            dx_drop_rows if dx_drop_rows is not None else dxl,
+                                            _d(drop_dx), _p(dsum), _stream()), "mmseq_layernorm_bwd_ex")
+        return
     if dx_drop_rows is not None:
         _check(lib().mmseq_layernorm_bwd_rows(nrows, cols, _p(dy), dyl, _p(x), xl, _p(mean), _p(rstd),
                                               _p(gamma), _p(dx), dxl, _p(dres), dresl, _p(dgamma),

@@ -373,7 +373,10 @@ constexpr int RPB16 = 64;
 // Q8 (config 5's fp8 dgrad): the gradient the next data-gradient GEMM reads (dxd when written, else
 // dx with the residual) also leaves in MX-fp8 (mmseq_quant_mxfp8 of the bf16 values: q [rows][ldq],
 // packed scales; the padding rows' scales are the caller's, zero-initialised)
-template <int NJ, bool DIN, bool DXD, bool Q8 = false>
+// CS: also the column sums of the gradient it writes for the next GEMM (dx_drop when DXD, else dx
+// with dres), as stored (bf16-rounded): the bias gradient of the Linear whose output gradient that
+// is, instead of a pass in its weight-gradient GEMM; per-block partials -> ws[block][2][cols]
+template <int NJ, bool DIN, bool DXD, bool Q8 = false, bool CS = false>
 __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, int rpb, const us* __restrict__ dy,
                                                        mmseq_rows dyl, const us* __restrict__ x,
                                                        mmseq_rows xl, const float* __restrict__ mean,
@@ -385,13 +388,18 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, int r
                                                        us* __restrict__ dxd, mmseq_rows dxdl, Drop dout,
                                                        uint8_t* __restrict__ q8 = nullptr,
                                                        int64_t ldq = 0, uint8_t* __restrict__ q8s = nullptr) {
-  __shared__ float red[4][2][NJ * 256];
+  constexpr int NA = CS ? 3 : 2;  // partial arrays: dgamma, dbeta (, the written gradient's sums)
+  __shared__ float red[4][NA][NJ * 256];
   const int l = threadIdx.x & 31, hw = threadIdx.x >> 5;
-  float pg[NJ][8], pb[NJ][8];
+  float pg[NJ][8], pb[NJ][8], pc[CS ? NJ : 1][8];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) pg[j][e] = pb[j][e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < (CS ? NJ : 1); ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pc[j][e] = 0.f;
   const int64_t rbeg = (int64_t)blockIdx.x * rpb;
   const int64_t rend = rbeg + rpb < rows ? rbeg + rpb : rows;
   auto load_g = [&](int c, float* g8) {
@@ -468,6 +476,12 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, int r
       }
       const u16x8 ob = pack8(o);
       *reinterpret_cast<u16x8*>(dxr + c) = ob;
+      if (CS) {
+        float t8[8];
+        unpack8(DXD ? qsrc : ob, t8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pc[j][e] += t8[e];
+      }
       if (Q8) {  // 32-column block = lanes l .. l + 3 (l & ~3): amax by two lane swaps
         if (!DXD) qsrc = ob;
         float qv[8], amax = 0.f;
@@ -507,6 +521,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, int r
       for (int e = 0; e < 8; ++e) {
         red[hw - 4][0][(j * 32 + l) * 8 + e] = pg[j][e];
         red[hw - 4][1][(j * 32 + l) * 8 + e] = pb[j][e];
+        if (CS) red[hw - 4][NA - 1][(j * 32 + l) * 8 + e] = pc[CS ? j : 0][e];
       }
   }
   __syncthreads();
@@ -517,14 +532,14 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(int rows, int cols, int r
       for (int e = 0; e < 8; ++e) {
         red[hw][0][(j * 32 + l) * 8 + e] += pg[j][e];
         red[hw][1][(j * 32 + l) * 8 + e] += pb[j][e];
+        if (CS) red[hw][NA - 1][(j * 32 + l) * 8 + e] += pc[CS ? j : 0][e];
       }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < cols; c += 256) {
-    const float g = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
-    const float b = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
-    ws[((int64_t)blockIdx.x * 2 + 0) * cols + c] = g;
-    ws[((int64_t)blockIdx.x * 2 + 1) * cols + c] = b;
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      ws[((int64_t)blockIdx.x * NA + k) * cols + c] = (red[0][k][c] + red[1][k][c]) + (red[2][k][c] + red[3][k][c]);
   }
 }
 
@@ -592,9 +607,20 @@ extern "C" mmseq_status mmseq_layernorm_fwd(int rows, int cols, const void* x, m
   return mmseq_check_launch("layernorm_fwd");
 }
 
+extern "C" int64_t mmseq_colsum_workspace(int rows, int cols);
+mmseq_status mmseq_reduce_partials3(int nb, int W, int split, int split2, const float* ws, float* ws2,
+                                    float* outA, float* outB, float* outC, int accumulate,
+                                    hipStream_t s);
+extern "C" mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t ldx, float* out,
+                                     int accumulate, float* ws, mmseq_dtype dt, mmseq_stream stream);
+
 extern "C" int64_t mmseq_layernorm_bwd_workspace(int rows, int cols) {
   const int nb = (rows + RPB16 - 1) / RPB16;  // the bf16 fast path's block count (>= the generic)
-  return (int64_t)nb * 2 * cols + mmseq_reduce_extra(nb, 2 * cols);
+  // three partial rows per block (dgamma, dbeta, the written gradient's column sums) or, where the
+  // fast kernel does not take the column sums, the separate column-sum pass's workspace
+  const int64_t w = (int64_t)nb * 3 * cols + mmseq_reduce_extra(nb, 3 * cols);
+  const int64_t c = mmseq_colsum_workspace(rows, cols);
+  return w > c ? w : c;
 }
 
 static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq_rows dyl,
@@ -604,10 +630,15 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
                                        float* dgamma, float* dbeta, float* workspace,
                                        mmseq_dtype dtype, const mmseq_dropout* drop_dy,
                                        void* dx_drop, mmseq_rows dxdl, const mmseq_dropout* drop_dx,
-                                       void* q, int64_t ldq, void* q_scales, mmseq_stream stream) {
+                                       void* q, int64_t ldq, void* q_scales, float* dsum,
+                                       mmseq_stream stream) {
   MMSEQ_REQUIRE(rows >= 0 && cols > 0 && cols <= 2048, "layernorm_bwd: cols must be in (0, 2048]");
   MMSEQ_REQUIRE(dy && x && mean && rstd && gamma && dx && workspace, "layernorm_bwd: null buffer");
   if (rows == 0) return MMSEQ_OK;
+  // dsum (+)= column sums of the gradient written for the next GEMM: dx_drop if given, else dx
+  const mmseq_rows gl = dx_drop ? dxdl : dxl;
+  MMSEQ_REQUIRE(!dsum || gl.rpb >= rows || gl.bstride == gl.rpb * gl.ld,
+                "layernorm_bwd: dsum needs the summed gradient in dense rows");
   if (!dres) dresl = dxl;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int nb = (rows + RPB - 1) / RPB;
@@ -627,6 +658,11 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
       nb16 = (rows + rpb - 1) / rpb;
     }
     const bool di = din.thr != 0, dd = dx_drop != nullptr;
+    // the column sums ride in the kernel where it has the registers (no input dropout, bf16 out)
+    const bool cs = dsum && !q && !di && cols <= 768;  // at cols 1024 it would spill
+#define LNB16C(NJ, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, false, B, false, true>), dim3(nb16), dim3(256), \
+                    0, s, rows, cols, rpb, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx,  \
+                    dxl, (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, nullptr, 0, nullptr)
 #define LNB16K(NJ, A, B) hipLaunchKernelGGL((ln_bwd16_kernel<NJ, A, B>), dim3(nb16), dim3(256), 0, s, rows, \
                     cols, rpb, (const us*)dy, dyl, (const us*)x, xl, mean, rstd, gamma, (us*)dx, dxl,         \
                     (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, nullptr, 0, nullptr)
@@ -635,6 +671,11 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
                     (const us*)dres, dresl, workspace, din, (us*)dx_drop, dxdl, dout, (uint8_t*)q, ldq, \
                     (uint8_t*)q_scales)
 #define LNB16(NJ)                                           \
+  if (cs) {                                                 \
+    if (dd) LNB16C(NJ, true);                               \
+    else LNB16C(NJ, false);                                 \
+  } else LNB16N(NJ)
+#define LNB16N(NJ)                                          \
   if (q) {                                                  \
     if (di && dd) LNB16Q(NJ, true, true);                   \
     else if (di) LNB16Q(NJ, true, false);                   \
@@ -646,14 +687,24 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
   else LNB16K(NJ, false, false);                            \
   break
     switch (cols / 256) {
-      case 1: LNB16(1); case 2: LNB16(2); case 3: LNB16(3); case 4: LNB16(4);
+      case 1: LNB16(1); case 2: LNB16(2); case 3: LNB16(3); case 4: LNB16N(4);
     }
 #undef LNB16
+#undef LNB16N
 #undef LNB16Q
 #undef LNB16K
+#undef LNB16C
     mmseq_status st = mmseq_check_launch("layernorm_bwd");
     if (st) return st;
-    if (dgamma || dbeta) return ln_reduce_partials(nb16, cols, workspace, dgamma, dbeta, s);
+    if (cs)
+      return mmseq_reduce_partials3(nb16, 3 * cols, cols, 2 * cols, workspace,
+                                    workspace + (int64_t)nb16 * 3 * cols, dgamma, dbeta, dsum, 1, s);
+    if (dgamma || dbeta) {
+      st = ln_reduce_partials(nb16, cols, workspace, dgamma, dbeta, s);
+      if (st) return st;
+    }
+    // column sums as their own pass over the written gradient (the workspace is free again)
+    if (dsum) return mmseq_colsum(rows, cols, dx_drop ? dx_drop : dx, gl.ld, dsum, 1, workspace, dtype, stream);
     return MMSEQ_OK;
   }
   if (q) return mmseq_set_error(MMSEQ_EUNSUPPORTED, "layernorm_bwd_mxfp8: bf16, cols 256..1024 (x256), 16-byte rows");
@@ -672,7 +723,11 @@ static mmseq_status layernorm_bwd_impl(int rows, int cols, const void* dy, mmseq
 #undef LNB
   mmseq_status st = mmseq_check_launch("layernorm_bwd");
   if (st) return st;
-  if (dgamma || dbeta) return ln_reduce_partials(nb, cols, workspace, dgamma, dbeta, s);
+  if (dgamma || dbeta) {
+    st = ln_reduce_partials(nb, cols, workspace, dgamma, dbeta, s);
+    if (st) return st;
+  }
+  if (dsum) return mmseq_colsum(rows, cols, dx_drop ? dx_drop : dx, gl.ld, dsum, 1, workspace, dtype, stream);
   return MMSEQ_OK;
 }
 
@@ -686,7 +741,21 @@ extern "C" mmseq_status mmseq_layernorm_bwd(int rows, int cols, const void* dy, 
                                             mmseq_stream stream) {
   return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
                             dgamma, dbeta, workspace, dtype, drop_dy, dx_drop, dxl, drop_dx, nullptr,
-                            0, nullptr, stream);
+                            0, nullptr, nullptr, stream);
+}
+
+extern "C" mmseq_status mmseq_layernorm_bwd_ex(int rows, int cols, const void* dy, mmseq_rows dyl,
+                                               const void* x, mmseq_rows xl, const float* mean,
+                                               const float* rstd, const float* gamma, void* dx,
+                                               mmseq_rows dxl, const void* dres, mmseq_rows dresl,
+                                               float* dgamma, float* dbeta, float* workspace,
+                                               mmseq_dtype dtype, const mmseq_dropout* drop_dy,
+                                               void* dx_drop, mmseq_rows dx_dropl,
+                                               const mmseq_dropout* drop_dx, float* dsum,
+                                               mmseq_stream stream) {
+  return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
+                            dgamma, dbeta, workspace, dtype, drop_dy, dx_drop,
+                            dx_drop ? dx_dropl : dxl, drop_dx, nullptr, 0, nullptr, dsum, stream);
 }
 
 extern "C" mmseq_status mmseq_layernorm_bwd_rows(int rows, int cols, const void* dy, mmseq_rows dyl,
@@ -700,7 +769,7 @@ extern "C" mmseq_status mmseq_layernorm_bwd_rows(int rows, int cols, const void*
   MMSEQ_REQUIRE(dx_drop, "layernorm_bwd_rows: dx_drop is required");
   return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
                             dgamma, dbeta, workspace, dtype, drop_dy, dx_drop, dx_dropl, drop_dx,
-                            nullptr, 0, nullptr, stream);
+                            nullptr, 0, nullptr, nullptr, stream);
 }
 
 extern "C" mmseq_status mmseq_layernorm_bwd_mxfp8(int rows, int cols, const void* dy, mmseq_rows dyl,
@@ -715,7 +784,7 @@ extern "C" mmseq_status mmseq_layernorm_bwd_mxfp8(int rows, int cols, const void
                 "layernorm_bwd_mxfp8: q / ldq");
   return layernorm_bwd_impl(rows, cols, dy, dyl, x, xl, mean, rstd, gamma, dx, dxl, dres, dresl,
                             dgamma, dbeta, workspace, MMSEQ_BF16, drop_dy, dx_drop, dxl, drop_dx, q,
-                            ldq, q_scales, stream);
+                            ldq, q_scales, nullptr, stream);
 }
 
 extern "C" mmseq_status mmseq_layernorm_fwd_mxfp8(int rows, int cols, const void* x, mmseq_rows xl,

@@ -240,6 +240,10 @@ class LayerRefs:
 # the last joint layer on the text rows only (BertLayerFn Tq); off (or MMSEQ_ROWS=0 in the
 # environment, for A/B runs): every layer over all T rows
 ROWS = {"on": os.environ.get("MMSEQ_ROWS", "1") != "0"}
+# the bias gradients of the two Linears whose output gradient a LayerNorm backward writes
+# (BertSelfOutput / BertOutput dense, the ViT out_proj) summed by that LN backward
+# (mmseq_layernorm_bwd_ex) instead of fused into their weight-gradient GEMMs; MMSEQ_LN_BIAS=0: fused
+LN_BIAS = {"on": os.environ.get("MMSEQ_LN_BIAS", "1") != "0"}
 
 
 # ================================================================================================
@@ -439,10 +443,14 @@ class BertLayerFn(torch.autograd.Function):
         ds2d = torch.empty_like(dy) if d_out is not None else ds2
         f8 = getattr(ctx, "f8dg", False)  # fp8 dgrad: the LN backwards also write the MX-fp8 operand
         lnb = N.layernorm_bwd_mxfp8 if f8 else N.layernorm_bwd
+        # bf16 / fp32: the LN backward also sums the gradient it writes for FC2 (BertOutput.dense's
+        # bias gradient), so the FC2 weight gradient runs without its fused bias pass
+        lnsum = LN_BIAS["on"] and not f8
+        bkw = {"dsum": st.g(L.out_b)} if lnsum else {}
         ds2q = lnb(R, H, dy, _rows(H), s2, _rows(H), m2, r2, st.f32(L.ln2_w), ds2, _rows(H),
                    None, _rows(H), st.g(L.ln2_w), st.g(L.ln2_b),
-                   dx_drop=ds2d if d_out is not None else None, drop_dx=d_out)
-        _wgrad(ds2d, gact, st.g(L.out_w), st.g(L.out_b))
+                   dx_drop=ds2d if d_out is not None else None, drop_dx=d_out, **bkw)
+        _wgrad(ds2d, gact, st.g(L.out_w), None if lnsum else st.g(L.out_b))
         dzq = None  # fp8 dgrad: FC2's dgrad epilogue writes FC1's dgrad operand in MX-fp8 as well
         if f8:
             dz, dzq = _dgrad8(ds2d, st, st.wt(L.out_w), act=GELU, dact=z, dyq=ds2q, q8=True)
@@ -460,15 +468,19 @@ class BertLayerFn(torch.autograd.Function):
             ds1d = torch.empty_like(dy)
             N.layernorm_bwd(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1,
                             N.rows(H, T * H, Tq), None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
-                            dx_drop=ds1d, drop_dx=d_o, dx_drop_rows=_rows(H))
+                            dx_drop=ds1d, drop_dx=d_o, dx_drop_rows=_rows(H),
+                            dsum=st.g(L.o_b) if lnsum else None)
             ds1q = None
         else:
             ds1 = torch.empty_like(dy)
             ds1d = torch.empty_like(dy) if d_o is not None else ds1
             ds1q = lnb(R, H, dh1, _rows(H), s1, _rows(H), m1, r1, st.f32(L.ln1_w), ds1, _rows(H),
                        None, _rows(H), st.g(L.ln1_w), st.g(L.ln1_b),
-                       dx_drop=ds1d if d_o is not None else None, drop_dx=d_o)
-        _wgrad(ds1d, o, st.g(L.o_w), st.g(L.o_b))
+                       dx_drop=ds1d if d_o is not None else None, drop_dx=d_o,
+                       **({"dsum": st.g(L.o_b)} if lnsum else {}))
+        # the attention output projection's bias gradient: summed by the LN backward above, or
+        # (fp8 dgrad) fused into its weight-gradient GEMM
+        _wgrad(ds1d, o, st.g(L.o_w), None if lnsum else st.g(L.o_b))
         do = _dgrad8(ds1d, st, st.wt(L.o_w), dyq=ds1q) if f8 else _dgrad(ds1d, st.wt(L.o_w))
         del ds1d
         dqkv = torch.empty_like(qkv)
@@ -606,10 +618,12 @@ class VitBlockFn(torch.autograd.Function):
         del dzq
         del dz
         dx1 = torch.empty_like(h)
+        # bf16 / fp32: out_proj's bias gradient = the column sums of dx1, taken by its LN backward
+        lnsum = LN_BIAS["on"] and not f8
         dx1q = (N.layernorm_bwd_mxfp8 if f8 else N.layernorm_bwd)(
             R, W, dhn2, _rows(W), x1, _rows(W), m2, r2, st.f32(L.ln2_w), dx1, _rows(W), dx2, _rows(W),
-            st.g(L.ln2_w), st.g(L.ln2_b))
-        _wgrad(dx1, o, st.g(L.out_w), st.g(L.out_b))
+            st.g(L.ln2_w), st.g(L.ln2_b), **({"dsum": st.g(L.out_b)} if lnsum else {}))
+        _wgrad(dx1, o, st.g(L.out_w), None if lnsum else st.g(L.out_b))
         do = dg(dx1, st.wt(L.out_w), dyq=dx1q) if f8 else _dgrad(dx1, st.wt(L.out_w))
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(P, heads, T, device=h.device)

@@ -265,6 +265,50 @@ def test_layernorm(dtype, rows, cols, eps):
     _close(db, rdb + 1, torch.float32, scale=10.0 if dtype == torch.float32 else 500.0)
 
 
+@pytest.mark.parametrize("dtype,rows,cols,mode", [
+    (torch.bfloat16, 70001, 768, "drop"),   # joint LN2 / LN1: sums of the masked copy (fast kernel)
+    (torch.bfloat16, 4099, 768, "dres"),    # ViT LN2: sums of dx with the residual (fast kernel)
+    (torch.bfloat16, 300, 256, "plain"),    # fast kernel, one 256-column chunk
+    (torch.bfloat16, 517, 1024, "drop"),    # cols 1024: the separate column-sum pass
+    (torch.float32, 333, 768, "drop"),      # fp32 parity mode: generic kernel + column-sum pass
+    (torch.bfloat16, 129, 96, "dres")])     # generic kernel (cols not a multiple of 256)
+def test_layernorm_bwd_column_sums(dtype, rows, cols, mode):
+    """mmseq_layernorm_bwd_ex: the LN backward outputs are unchanged and dsum accumulates the
+    column sums of the gradient it writes for the next GEMM (dx_drop, else dx with dres), as stored;
+    bitwise repeatable."""
+    g = torch.Generator(device="cpu").manual_seed(rows * 3 + cols)
+    x = (torch.randn(rows, cols, generator=g) * 2 + 0.5).to(DEV, dtype)
+    gamma = (1 + 0.1 * torch.randn(cols, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(cols, generator=g)).to(DEV)
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    nat.layernorm_fwd(rows, cols, x, nat.rows(cols), gamma, beta, 1e-12, y, nat.rows(cols), mean, rstd)
+    dy = torch.randn(rows, cols, generator=g).to(DEV, dtype)
+    dres = torch.randn(rows, cols, generator=g).to(DEV, dtype) if mode == "dres" else None
+    d = nat.drop(0.1, 7, 11) if mode == "drop" else None
+
+    def run(dsum):
+        dx, dxd = torch.empty_like(x), torch.empty_like(x) if d is not None else None
+        dg, db = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+        nat.layernorm_bwd(rows, cols, dy, nat.rows(cols), x, nat.rows(cols), mean, rstd, gamma, dx,
+                          nat.rows(cols), dres, nat.rows(cols), dg, db, dx_drop=dxd, drop_dx=d,
+                          dsum=dsum)
+        return dx, dxd, dg, db
+
+    dx0, dxd0, dg0, db0 = run(None)
+    acc = torch.full((cols,), 0.5, device=DEV)
+    dx1, dxd1, dg1, db1 = run(acc)
+    assert torch.equal(dx1, dx0) and (dxd0 is None or torch.equal(dxd1, dxd0))
+    torch.testing.assert_close(dg1, dg0, rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(db1, db0, rtol=1e-6, atol=1e-5)
+    summed = (dxd0 if dxd0 is not None else dx0).double().sum(0)
+    tol = 1e-6 * float(summed.abs().max()) + 1e-3
+    assert float((acc.double() - 0.5 - summed).abs().max()) < tol
+    acc2 = torch.full((cols,), 0.5, device=DEV)
+    run(acc2)
+    assert torch.equal(acc2, acc)
+
+
 def test_layernorm_strided_rows():
     # write the visual half of a [P][T][H] joint buffer in place (two-level strides)
     P, Lt, Tv, H = 3, 5, 7, 64

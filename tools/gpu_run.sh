@@ -15,6 +15,7 @@
 #   epi-ab:NAME      tools/gemm_epi_bench.py, NAME vs tree, twice     -> epi_{NAME,tree}.log
 #   bench-ab:NAME    short bench (config 3 only), NAME vs tree, twice -> bench_{NAME,tree}.log
 #   kstats:SCRIPT ARGS  rocprof kernel stats of python SCRIPT ARGS    -> <script>_stats.csv
+#   kstats-env:VAR=VAL:SCRIPT ARGS  the same with VAR=VAL exported   -> <script>_VAR<VAL>_stats.csv
 #   env-ab:VAR[:SCRIPT ARGS]  the short config-3 bench (or python SCRIPT ARGS) with VAR=0 vs VAR=1,
 #                    alternated twice (e.g. env-ab:MMSEQ_ROWS, env-ab:MMSEQ_ROWS:tools/c5_train.py bf16 3)
 #                                                                     -> envab_VAR{0,1}.log
@@ -76,6 +77,12 @@ for step in "$@"; do
     kstats)
       s=$(basename "${arg%% *}" .py)
       kstats "$out/${s}_stats.csv" $arg ;;
+    kstats-env)
+      kv=${arg%%:*}; cmd=${arg#*:}
+      s=$(basename "${cmd%% *}" .py)
+      export "${kv?}"
+      kstats "$out/${s}_${kv%%=*}${kv#*=}_stats.csv" $cmd
+      unset "${kv%%=*}" ;;
     env-ab)
       var=${arg%%:*}; cmd=""
       [ "$var" != "$arg" ] && cmd=${arg#*:}
