@@ -333,6 +333,12 @@ mmseq_status mmseq_cast(int64_t n, const void* src, mmseq_dtype src_dtype, void*
 /* dst[c][r] = src[r][c] for an f32 [rows][cols] matrix, written as dst_dtype */
 mmseq_status mmseq_transpose_cast(int rows, int cols, const float* src, void* dst,
                                   mmseq_dtype dst_dtype, mmseq_stream stream);
+/* transpose_cast_batch: n fp32 matrices transposed (and cast) in one launch: desc[5*m ..] = {rows,
+ *  cols, src offset, dst offset, first tile} in elements of src / dst, tiles of 64 x 64 numbered
+ *  matrix by matrix (first tile of m = sum of ceil(rows/64)*ceil(cols/64) before it), tiles = the
+ *  total; desc in device memory. The per-step refresh of a store's transposed dgrad shadows. */
+mmseq_status mmseq_transpose_cast_batch(int n, const int64_t* desc, int64_t tiles, const float* src,
+                                        void* dst, mmseq_dtype dd, mmseq_stream stream);
 /* out[c] (+)= sum_r x[r][c] in f32 (bias gradients); rows at x + r*ldx. */
 mmseq_status mmseq_colsum(int rows, int cols, const void* x, int64_t ldx, float* out,
                           int accumulate, float* workspace, mmseq_dtype dtype,

@@ -128,6 +128,8 @@ _SIGS = {
     "mmseq_vit_embed_bwd": (ctypes.c_int, [ctypes.c_int] * 4 + [_vp] * 11 + [ctypes.c_int, _vp]),
     "mmseq_vit_embed_bwd_workspace": (ctypes.c_int64, [ctypes.c_int] * 3),
     "mmseq_cast": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp]),
+    "mmseq_transpose_cast_batch": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, ctypes.c_int,
+                                                  _vp]),
     "mmseq_transpose_cast": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, ctypes.c_int,
                                             _vp]),
     "mmseq_colsum": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _c_i64, _vp, ctypes.c_int,
@@ -464,6 +466,14 @@ def cast(src, dst):
     assert src.numel() == dst.numel()
     _check(lib().mmseq_cast(src.numel(), _p(src), dt(src), _p(dst), dt(dst), _stream()),
            "mmseq_cast")
+
+
+def transpose_cast_batch(desc, tiles, src, dst):
+    """desc: int64 device tensor [n][5] = (rows, cols, src offset, dst offset, first 64x64 tile)
+    of fp32 matrices in src (flat), transposed into dst (flat, dst's dtype)."""
+    _dev(desc, src, dst)
+    _check(lib().mmseq_transpose_cast_batch(desc.shape[0], _p(desc), tiles, _p(src), _p(dst), dt(dst),
+                                            _stream()), "mmseq_transpose_cast_batch")
 
 
 def transpose_cast(src, dst):

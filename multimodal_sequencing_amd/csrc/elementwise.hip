@@ -31,6 +31,59 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
   }
 }
 
+// Many fp32 [rows][cols] matrices -> their bf16 / fp32 transposes in one launch (the per-step
+// refresh of a parameter store's transposed dgrad shadows): desc[m] = {rows, cols, src offset,
+// dst offset, first tile} (elements; 64 x 64 tiles numbered matrix by matrix), one workgroup per
+// tile, 16-byte fp32 reads along a source row, 8-byte writes along a destination row.
+template <typename TD>
+__global__ __launch_bounds__(256) void transpose_batch_kernel(int n, const int64_t* __restrict__ desc,
+                                                              const float* __restrict__ src,
+                                                              TD* __restrict__ dst) {
+  __shared__ float t[64][65];
+  const int64_t tile = blockIdx.x;
+  int lo = 0, hi = n - 1;  // the last matrix whose first tile <= this tile (uniform)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid * 5 + 4] <= tile) lo = mid; else hi = mid - 1;
+  }
+  const int rows = (int)desc[lo * 5], cols = (int)desc[lo * 5 + 1];
+  const float* s = src + desc[lo * 5 + 2];
+  TD* d = dst + desc[lo * 5 + 3];
+  const int tc = (cols + 63) >> 6;
+  const int64_t k = tile - desc[lo * 5 + 4];
+  const int r0 = (int)(k / tc) * 64, c0 = (int)(k % tc) * 64;
+  const int tid = threadIdx.x;
+  const bool vec = (cols & 3) == 0 && (desc[lo * 5 + 2] & 3) == 0;  // 16-byte aligned source rows
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {  // 64 rows x 16 quads, 16 rows per pass
+    const int rr = p * 16 + (tid >> 4), cq = (tid & 15) * 4;
+    const int r = r0 + rr, c = c0 + cq;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < rows) {
+      if (vec && c + 3 < cols) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(s + (int64_t)r * cols + c);
+        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+      } else {
+        for (int e = 0; e < 4; ++e)
+          if (c + e < cols) v[e] = s[(int64_t)r * cols + c + e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[rr][cq + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {  // destination row = source column c0 + cc, 4 source rows per lane
+    const int cc = p * 16 + (tid >> 4), rq = (tid & 15) * 4;
+    const int c = c0 + cc, r = r0 + rq;
+    if (c >= cols) continue;
+    TD* o = d + (int64_t)c * rows + r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (r + e < rows) Elem<TD>::st(o + e, t[rq + e][cc]);
+  }
+}
+
 constexpr int CS_ROWS = 256;
 // partial column sums over CS_ROWS rows: lane owns 8 columns (16-byte bf16 loads when VEC),
 // the 4 waves of the block stride over the rows and are combined through LDS.
@@ -179,6 +232,21 @@ extern "C" mmseq_status mmseq_transpose_cast(int rows, int cols, const float* sr
     hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, s, rows, cols, src,
                        (float*)dst);
   return mmseq_check_launch("transpose_cast");
+}
+
+extern "C" mmseq_status mmseq_transpose_cast_batch(int n, const int64_t* desc, int64_t tiles,
+                                                   const float* src, void* dst, mmseq_dtype dd,
+                                                   mmseq_stream stream) {
+  MMSEQ_REQUIRE(n >= 0 && tiles >= 0 && (n == 0 || (desc && src && dst)), "transpose_cast_batch: bad args");
+  if (!n || !tiles) return MMSEQ_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dd == MMSEQ_BF16)
+    hipLaunchKernelGGL(transpose_batch_kernel<unsigned short>, dim3((unsigned)tiles), dim3(256), 0, s, n,
+                       desc, src, (unsigned short*)dst);
+  else
+    hipLaunchKernelGGL(transpose_batch_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, n, desc,
+                       src, (float*)dst);
+  return mmseq_check_launch("transpose_cast_batch");
 }
 
 int64_t mmseq_reduce_extra(int nb, int W);

@@ -157,13 +157,27 @@ class ParamStore:
     def zero_grad(self):
         self.grad.zero_()
 
+    def refresh_transposes(self):
+        """Every transposed shadow from the master weights in one launch
+        (mmseq_transpose_cast_batch; the descriptor table is built once)."""
+        if not self.t_offsets:
+            return
+        if getattr(self, "_tdesc", None) is None:
+            rows_desc, tiles = [], 0
+            for first, (t, names) in self.t_offsets.items():
+                rows = sum(self._spec(x).shape[0] for x in names)
+                cols = _numel(self._spec(first).shape) // self._spec(first).shape[0]
+                rows_desc.append([rows, cols, self.offsets[first], t, tiles])
+                tiles += ((rows + 63) // 64) * ((cols + 63) // 64)
+            self._tdesc = torch.tensor(rows_desc, dtype=torch.int64, device=self.device)
+            self._ttiles = tiles
+        N.transpose_cast_batch(self._tdesc, self._ttiles, self.master, self.shadow_t)
+
     def refresh_shadows(self):
         """Re-derive the compute-dtype shadows from the master weights (after every update)."""
         if self.compute_dtype != torch.float32:
             N.cast(self.master, self.shadow)
-        for first, (t, names) in self.t_offsets.items():
-            src = self.packed(names, "f32")
-            N.transpose_cast(src, self.shadow_t[t:t + src.numel()])
+        self.refresh_transposes()
         self.shadow_stale = False
         self.version += 1
 

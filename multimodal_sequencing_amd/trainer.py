@@ -81,9 +81,7 @@ class FusedAdamW:
             s.version += 1
             if s.compute_dtype == torch.bfloat16:
                 s.shadow_stale = False
-                for first, (t, names) in s.t_offsets.items():
-                    src = s.packed(names, "f32")
-                    N.transpose_cast(src, s.shadow_t[t:t + src.numel()])
+                s.refresh_transposes()
             else:
                 s.refresh_shadows()
         return lr

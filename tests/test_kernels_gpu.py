@@ -309,6 +309,27 @@ def test_layernorm_bwd_column_sums(dtype, rows, cols, mode):
     assert torch.equal(acc2, acc)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_transpose_cast_batch(dtype):
+    """mmseq_transpose_cast_batch: several fp32 matrices (ragged edges, odd widths, an unaligned
+    source offset) transposed into one flat buffer in one launch, exactly as the cast of their
+    transposes."""
+    shapes = [(768, 768), (2304, 768), (130, 70), (1, 5), (3072, 768), (64, 3), (97, 128)]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    src = torch.randn(sum(r * c for r, c in shapes) + 64 * len(shapes) + 2, generator=g).to(DEV)
+    dst = torch.full((sum(r * c for r, c in shapes) + 64 * len(shapes),), 7.0, device=DEV, dtype=dtype)
+    desc, so, do_, tiles = [], 2, 0, 0  # source offset 2: the unaligned (scalar) path
+    for r, c in shapes:
+        desc.append([r, c, so, do_, tiles])
+        tiles += ((r + 63) // 64) * ((c + 63) // 64)
+        so += r * c + (64 if so % 64 == 0 else 62)
+        do_ += r * c + 64
+    nat.transpose_cast_batch(torch.tensor(desc, dtype=torch.int64, device=DEV), tiles, src, dst)
+    for (r, c, so, do_, _) in desc:
+        want = src[so:so + r * c].view(r, c).t().contiguous().to(dtype)
+        assert torch.equal(dst[do_:do_ + r * c].view(c, r), want)
+
+
 def test_layernorm_strided_rows():
     # write the visual half of a [P][T][H] joint buffer in place (two-level strides)
     P, Lt, Tv, H = 3, 5, 7, 64
