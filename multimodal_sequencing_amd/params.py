@@ -12,6 +12,7 @@ Drop-in surface: `named_parameters()` / `state_dict()` expose the reference's ke
 view is the matching slice of the grad buffer.
 """
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -161,6 +162,11 @@ class ParamStore:
         """Every transposed shadow from the master weights in one launch
         (mmseq_transpose_cast_batch; the descriptor table is built once)."""
         if not self.t_offsets:
+            return
+        if os.environ.get("MMSEQ_TBATCH", "1") == "0":  # A/B: one launch per matrix
+            for first, (t, names) in self.t_offsets.items():
+                src = self.packed(names, "f32")
+                N.transpose_cast(src, self.shadow_t[t:t + src.numel()])
             return
         if getattr(self, "_tdesc", None) is None:
             rows_desc, tiles = [], 0
