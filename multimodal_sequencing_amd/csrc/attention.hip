@@ -45,7 +45,9 @@ struct AttnArgs {
   int nkt2;        // key tiles per row, rounded up to even (16-byte rows for the dK/dV staging)
   // tail fold (bf16 dK/dV kernel): when 1 <= T % 128 <= 16 the last 128-row block of each (pair,
   // head) also owns rows tail0 .. T-1 (tail0 = 128 * (T / 128)); 0 = no fold. nxq = row blocks.
-  int tail0, nxq;
+  // dK/dV launches: blocks x = xoff .. xoff + nxl - 1 of every (pair, head) (the tail block runs in
+  // a launch of its own, so the other blocks' kernel carries no tail state)
+  int tail0, nxq, xoff, nxl;
   // query rows per pair (bf16 fast kernels; the other kernels take Tq == T): queries 0 .. Tq-1 of
   // every pair against all T keys; O / dO hold Tq rows per pair (row p * Tq + q)
   int Tq;
@@ -1732,7 +1734,10 @@ __device__ __forceinline__ void zero_dq(const AttnArgs& a, unsigned short* row, 
 }
 
 // ---- backward: dK, dV (per 128-key block, queries swept; key on the MFMA lane) ----------------
-template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
+// FOLD: this launch holds the tail blocks (x = nxq - 1 when a.tail0 > 0); the kernel without it
+// carries none of the tail keys' registers (dK/dV<2>: 251 -> 212 VGPRs, <0>: 234 -> 166, i.e. three
+// waves per SIMD instead of two)
+template <int DMODE, bool FOLD>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
 __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (Q, dO) + lse, D
@@ -1749,7 +1754,8 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
-  const BlkIdx bi = attn_block(a.nxq, a.heads);
+  BlkIdx bi = attn_block(a.nxl, a.heads);
+  bi.x += a.xoff;
   const int h = bi.h, p = bi.p;
   const int kw = bi.x * 128 + wave * 32;
   const bool active = kw < T;
@@ -1757,7 +1763,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   // split over the waves (wave w takes the 16-query block w of every tile) and the four partial
   // dK / dV tiles are summed in wave order at the end (deterministic); not in the counter-hash mode
   // (DMODE 1: its registers go to the hashed keep masks; the host does not fold it)
-  const bool tailb = DMODE != 1 && a.tail0 > 0 && bi.x == a.nxq - 1;
+  const bool tailb = FOLD && DMODE != 1 && a.tail0 > 0 && bi.x == a.nxq - 1;
   const int64_t ld = a.ld_qkv;
   const rsrc_t rq = head_rsrc(a.qkv, (int64_t)p * T, ld, a.q_off + h * 64, T);
   const rsrc_t ro = head_rsrc(a.dout, (int64_t)p * Tq, a.ld_dout, h * 64, Tq);
@@ -2226,17 +2232,37 @@ static mmseq_status attn_bwd_impl(int P, int T, int Tq, int heads, const void* q
     // the dQ kernel does not fold: its tail state took it from three to two waves per SIMD
     // (148 -> 236 VGPRs), slower at T = 513 and 393 than the extra block it saves
     tail_fold(a, 0);
-    const dim3 gdq((unsigned)(((Tq + 127) / 128) * heads * P)), gdk((unsigned)(ak.nxq * heads * P));
+    const dim3 gdq((unsigned)(((Tq + 127) / 128) * heads * P));
+    // dK/dV: the blocks without the tail keys in one launch, the tail blocks (x = nxq - 1 when
+    // folded) in a second one with the fold's state and LDS
+    const int nplain = ak.tail0 ? ak.nxq - 1 : ak.nxq;
+    AttnArgs akt = ak;
+    ak.xoff = 0; ak.nxl = nplain;
+    akt.xoff = nplain; akt.nxl = 1;
+    const dim3 gdk((unsigned)(nplain * heads * P)), gdt((unsigned)(heads * P));
+#ifdef MMSEQ_ATTN_ONE_DKDV  // A/B: every block in the FOLD kernel (one launch)
+    ak.nxl = ak.nxq; const int ntail = 0;
+    const dim3 gdk1((unsigned)(ak.nxq * heads * P));
+#define DKDV_PLAIN(D) hipLaunchKernelGGL((attn_dkdv_bf16_kernel<D, true>), gdk1, dim3(256), ldsk, s, ak)
+#else
+    const int ntail = ak.tail0 ? 1 : 0;
+#define DKDV_PLAIN(D) if (nplain) hipLaunchKernelGGL((attn_dkdv_bf16_kernel<D, false>), gdk, dim3(256), lds, s, ak)
+#endif
+#define DKDV_TAIL(D) if (ntail) hipLaunchKernelGGL((attn_dkdv_bf16_kernel<D, true>), gdt, dim3(256), ldsk, s, akt)
     if (dmode == 2) {
       hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gdq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<2>, gdk, dim3(256), ldsk, s, ak);
+      DKDV_PLAIN(2);
+      DKDV_TAIL(2);
     } else if (dmode == 1) {
       hipLaunchKernelGGL(attn_dq_bf16_kernel<1>, gdq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<1>, gdk, dim3(256), ldsk, s, ak);
+      DKDV_PLAIN(1);  // the counter-hash mode never folds
     } else {
       hipLaunchKernelGGL(attn_dq_bf16_kernel<0>, gdq, dim3(256), lds, s, a);
-      hipLaunchKernelGGL(attn_dkdv_bf16_kernel<0>, gdk, dim3(256), ldsk, s, ak);
+      DKDV_PLAIN(0);
+      DKDV_TAIL(0);
     }
+#undef DKDV_PLAIN
+#undef DKDV_TAIL
   } else if (dtype == MMSEQ_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<unsigned short>, gd, dim3(256), 0, s, a);
     hipLaunchKernelGGL(attn_dkdv_kernel<unsigned short>, grid, dim3(256), 0, s, a);

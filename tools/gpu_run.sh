@@ -21,6 +21,8 @@
 #                                                                     -> envab_VAR{0,1}.log
 #   lib-ab:NAME:SCRIPT ARGS  python SCRIPT ARGS with ab/libmmseq_NAME.so vs the tree, alternated
 #                    twice (e.g. lib-ab:base:tools/ln_bench.py bwd)   -> <script>_{NAME,tree}.log
+#   pmc:NAME:CTRS:SCRIPT ARGS  one rocprofv3 --pmc pass (CTRS space-free, comma-separated, within
+#                    the per-block limits) over python SCRIPT ARGS  -> pmc_NAME.csv
 #   profile          tools/profile_round.sh TAG (kernel stats + PMC of the default bench)
 #   dp2-gloo         the 2-rank data-parallel path on this one GPU over gloo (4 stories per rank,
 #                    the bench line with its all-reduce diagnostics) -> bench_dp2_gloo.log
@@ -102,6 +104,13 @@ for step in "$@"; do
         timeout -k 10 300 python3 $cmd >> "$out/${s}_$v.log" 2>&1
       done
       unset MMSEQ_BENCH_LIB ;;
+    pmc)
+      pn=${arg%%:*}; rest=${arg#*:}; ctrs=${rest%%:*}; cmd=${rest#*:}
+      d="$out/pmc_$$"
+      timeout -s KILL 120 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d "$d" -o pm -- \
+        python3 $cmd >> "$out/pmc_$pn.log" 2>&1
+      cat "$(find "$d" -name 'pm_counter_collection.csv' | head -n1)" > "$out/pmc_$pn.csv"
+      rm -rf "$d" ;;
     profile)
       bash tools/profile_round.sh "$tag" ;;
     dp2-gloo)
