@@ -1737,8 +1737,17 @@ __device__ __forceinline__ void zero_dq(const AttnArgs& a, unsigned short* row, 
 // FOLD: this launch holds the tail blocks (x = nxq - 1 when a.tail0 > 0); the kernel without it
 // carries none of the tail keys' registers (dK/dV<2>: 251 -> 212 VGPRs, <0>: 234 -> 166, i.e. three
 // waves per SIMD instead of two)
+// Plain blocks of the keep-bit / no-dropout modes: three workgroups per CU (<= 168 VGPRs); in the
+// keep-bit one the lane-derived LDS offsets are recomputed in every tile (volatile lane copy) rather
+// than held across the loop, which at 168 registers spilled them into reloads whose vmcnt wait also
+// drained the next tile's DMA. MMSEQ_DKDV_WG2: the two-workgroup bound for every instantiation (A/B).
+#ifdef MMSEQ_DKDV_WG2
+#define DKDV_WG(FOLD, D) 2
+#else
+#define DKDV_WG(FOLD, D) ((FOLD) || (D) == 1 ? 2 : 3)
+#endif
 template <int DMODE, bool FOLD>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
-__global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DKDV_WG(FOLD, DMODE)) void attn_dkdv_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (Q, dO) + lse, D
   const int T = a.T, Tq = a.Tq;
@@ -1859,10 +1868,6 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
   } else {
     kb2t = -1e30f;
   }
-  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
-  int to[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
   const int Tp4 = (T + 3) & ~3;
   f32x4 dk[2][4], dv[2][4], dkt[4], dvt[4];
@@ -1880,6 +1885,15 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_bf16_kernel(AttnArgs a) {
     if (!active) continue;
     const unsigned short* qimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* oimg = qimg + IMG;
+    int ro0, ro1, to[4];
+    {
+      uint32_t ln = (uint32_t)lane;  // the 3-workgroup keep-bit kernel: not hoisted out of the loop
+      if (DMODE == 2 && !FOLD) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(ln));
+      ro0 = row_off((int)ln, 0);
+      ro1 = row_off((int)ln, 1);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) to[d] = tr_off((int)ln, d);
+    }
     // dropout multiplier of element (grp, qs, r): 0 or 1/(1-p), as the bits of the scale ANDed with
     // a sign-extended 1-bit field (v_bfe_i32 + v_and per element)
     const uint32_t scale_u = __float_as_uint(a.drop.scale);
