@@ -1538,8 +1538,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ---- backward: dQ (per 128-query block, keys swept), also writes delta = rowsum(dO * O) --------
+// without dropout four workgroups per CU (127 VGPRs); the dropout modes need 142-148 (three)
 template <int DMODE>  // dropout: 0 none, 1 counter hash, 2 keep bits from the forward
-__global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DMODE == 0 ? 4 : 2) void attn_dq_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
   float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
@@ -1623,10 +1624,6 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     settle(qf[grp][1]);
     settle(L2[grp]);
   }
-  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
-  int to[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
   const int Tp4 = (T + 3) & ~3;
   uint64_t drow[2];
@@ -1663,6 +1660,16 @@ __global__ __launch_bounds__(256, 2) void attn_dq_bf16_kernel(AttnArgs a) {
     if (!active) continue;
     const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* vimg = kimg + IMG;
+    int ro0, ro1, to[4];
+    {
+      uint32_t ln = (uint32_t)lane;  // no dropout (four workgroups per CU, <= 128 VGPRs): the lane-
+      // derived LDS offsets are recomputed per tile instead of held across the loop
+      if (DMODE == 0) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(ln));
+      ro0 = row_off((int)ln, 0);
+      ro1 = row_off((int)ln, 1);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) to[d] = tr_off((int)ln, d);
+    }
     f32x4 s[2][4], dp[2][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -2235,6 +2242,8 @@ static mmseq_status attn_bwd_impl(int P, int T, int Tq, int heads, const void* q
                   "attn_bwd: out / dqkv must be 16-byte aligned rows");
     const dim3 gq((unsigned)(((T + 127) / 128) * heads * P));
     const size_t lds = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4 * 2 + 2048;
+    // dQ: K / V double buffer + the key-bias row (four workgroups per CU without dropout)
+    const size_t ldsq = (size_t)4 * 4096 * 2 + (size_t)((T + 63) / 64) * 64 * 4;
     a.bits = const_cast<uint64_t*>(keep_bits);
     a.nkt2 = (((T + 63) / 64) + 1) & ~1;
     // dK/dV tail fold: + the tail keys' keep words (2 KB) and K / V fragments (4 KB); the counter-
@@ -2264,14 +2273,14 @@ static mmseq_status attn_bwd_impl(int P, int T, int Tq, int heads, const void* q
 #endif
 #define DKDV_TAIL(D) if (ntail) hipLaunchKernelGGL((attn_dkdv_bf16_kernel<D, true>), gdt, dim3(256), ldsk, s, akt)
     if (dmode == 2) {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gdq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<2>, gdq, dim3(256), ldsq, s, a);
       DKDV_PLAIN(2);
       DKDV_TAIL(2);
     } else if (dmode == 1) {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<1>, gdq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<1>, gdq, dim3(256), ldsq, s, a);
       DKDV_PLAIN(1);  // the counter-hash mode never folds
     } else {
-      hipLaunchKernelGGL(attn_dq_bf16_kernel<0>, gdq, dim3(256), lds, s, a);
+      hipLaunchKernelGGL(attn_dq_bf16_kernel<0>, gdq, dim3(256), ldsq, s, a);
       DKDV_PLAIN(0);
       DKDV_TAIL(0);
     }
