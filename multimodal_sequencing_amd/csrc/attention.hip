@@ -938,7 +938,10 @@ template <int DMODE, bool WIDE, bool Q8 = false>  // dropout: 0 none, 1 counter 
 #ifndef MMSEQ_ATTN_FWD_WPE
 #define MMSEQ_ATTN_FWD_WPE 3  // forward workgroups per CU the register budget is sized for
 #endif
-__global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(AttnArgs a) {
+// (without dropout: four, <= 128 VGPRs, with the lane-derived LDS and DMA offsets recomputed in the
+// loop from a volatile lane copy instead of held across it; the spilled remainder is reloaded after
+// the loop)
+__global__ __launch_bounds__(256, DMODE == 0 ? 4 : MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(AttnArgs a) {
   constexpr bool DROP = DMODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];  // 2 x (K, V) + bias
   float* sBias = reinterpret_cast<float*>(smem + 4 * IMG);
@@ -969,10 +972,16 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
   const uint32_t boff0 = (uint32_t)(((qw + i) * a.nkt2 * 4 + g) * 2);
   auto stage = [&](int t) {
     unsigned short* kimg = smem + (t & 1) * 2 * IMG;
+    uint32_t lo = loff;
+    if (DMODE == 0) {  // recomputed per call (a volatile lane copy), not held across the loop
+      uint32_t ln = (uint32_t)lane;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(ln));
+      lo = dma_lane_off((int)ln, ld);
+    }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int pc = wave * 2 + e;
-      const uint32_t vo = loff + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2);
+      const uint32_t vo = lo + (uint32_t)((int64_t)(t * 64 + pc * 8) * ld * 2);
       dma16(rk, kimg + pc * 512, vo);
       dma16(rv, kimg + IMG + pc * 512, vo);
     }
@@ -1008,10 +1017,6 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) settle(qf[grp][ks]);
 
-  const int ro0 = row_off(lane, 0), ro1 = row_off(lane, 1);
-  int to[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) to[d] = tr_off(lane, d);
   const float c = a.scale * LOG2E;
   const int Tp4 = (T + 3) & ~3;
   uint64_t drow[2];
@@ -1045,6 +1050,15 @@ __global__ __launch_bounds__(256, MMSEQ_ATTN_FWD_WPE) void attn_fwd_bf16_kernel(
     if (!active) continue;
     const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* vimg = kimg + IMG;
+    int ro0, ro1, to[4];
+    {
+      uint32_t ln = (uint32_t)lane;
+      if (DMODE == 0) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(ln));
+      ro0 = row_off((int)ln, 0);
+      ro1 = row_off((int)ln, 1);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) to[d] = tr_off((int)ln, d);
+    }
     // 16-key blocks holding a valid key (the last tile of T = 64n + 1 has one): the others are
     // all masked (p = 0), so their MFMAs and softmax work are skipped
     const int nkb = t == nkt - 1 ? min(4, (T - t * 64 + 15) >> 4) : 4;
