@@ -1671,6 +1671,9 @@ __global__ __launch_bounds__(256, DMODE == 0 ? 4 : 2) void attn_dq_bf16_kernel(A
       for (int grp = 0; grp < 2; ++grp)
         kwn[grp] = __builtin_amdgcn_raw_buffer_load_b16(rbits, boff0 + grp * 16 * a.nkt2 * 8 + (t + 1) * 8, 0, 0);
     }
+    // issued here, a whole tile ahead of the wait at the next tile's top (left to the scheduler they
+    // sank to the end of the tile body, and that wait then exposed their memory latency)
+    if (DMODE == 2) __builtin_amdgcn_sched_barrier(0);
     if (!active) continue;
     const unsigned short* kimg = smem + (t & 1) * 2 * IMG;
     const unsigned short* vimg = kimg + IMG;
